@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""bench.py -- nnz(C)/s of R-MAT A*A through the MI355X 2D-SUMMA SpGEMM path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--algo doublebuff|synch]
+                  [--exec panel|staged] [--no-cpu-baseline]
+
+One step = one complete Mult_AnXBn_DoubleBuff (reference ParFriends.h:798-997)
+of Graph500 R-MAT A (SEED 0xDECAFBAD, ef 16, duplicates summed, loops removed)
+by a deep copy of A, inputs resident in HBM in the 2D block layout, C left
+resident per tile.  N=1 runs the largest configuration that fits one GPU
+(configs[1]: scale 18 by default).  N>1: launched by torch.distributed.run, one
+rank per GPU, RCCL row/column communicators (grid 1x2, 2x2, 2x4 for 2/4/8).
+
+Prints ONE JSON line on rank 0 (see the driver contract in DESIGN.md).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def load_cbg():
+    import importlib.util
+    name = "combblas_spmm_test_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REPO, "combblas-spmm-test_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+GRIDS = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 9: (3, 3), 16: (4, 4)}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scale", type=int, default=None)
+    p.add_argument("--ef", type=int, default=16)
+    p.add_argument("--seed", type=lambda s: int(s, 0), default=0xDECAFBAD)
+    p.add_argument("--algo", choices=["doublebuff", "synch"], default="doublebuff")
+    p.add_argument("--exec", dest="exec_mode", choices=["panel", "staged"], default="panel")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-scale", type=int, default=None, help="scale of the CPU-baseline sample")
+    return p.parse_args()
+
+
+def cpu_baseline(scale, ef, seed, threads):
+    """Oracle (plain-C restatement of the reference MPI+OpenMP path) timed on host cores.
+
+    Times Mult_AnXBn_Synch and Mult_AnXBn_DoubleBuff restated (oracle/cbg_oracle.c)
+    at 1x1 on `threads` OpenMP threads and reports the better one."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from helpers import oracle_rmat, oracle_summa  # test infrastructure: the checker/baseline only
+    A = oracle_rmat(scale, ef, seed, threads)
+    B = dict(A)
+    best = None
+    for algo in ("synch", "doublebuff"):
+        t0 = time.perf_counter()
+        C = oracle_summa(A, B, 1, algo, "plus", threads)
+        dt = time.perf_counter() - t0
+        nnz = len(C["ir"])
+        del C
+        r = nnz / dt
+        if best is None or r > best[0]:
+            best = (r, algo, dt, nnz)
+    return best
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    N = max(world, 1)
+    scale = a.scale if a.scale is not None else (18 if N == 1 else 22)
+    cbg = load_cbg()  # libcbg first: its HIP/RCCL runtimes are the ones the process uses
+    cbg.lib().cbg_set_device(local_rank)
+
+    if N == 1:
+        class Self:
+            def bcast(self, comm, arr, root):
+                pass
+
+            def allgather(self, comm, data):
+                return data
+
+        grid = cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+    else:
+        import torch.distributed as dist  # bootstrap only (gloo, host side)
+        dist.init_process_group("gloo")
+        uid = [cbg.CommGrid.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pr, pc = GRIDS[N]
+        grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid[0], transport="rccl")
+
+    t_gen = time.perf_counter()
+    A = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)
+    B = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)  # deep copy (aliasing is forbidden)
+    cbg.synchronize()
+    t_gen = time.perf_counter() - t_gen
+    mult = cbg.Mult_AnXBn_DoubleBuff if a.algo == "doublebuff" else cbg.Mult_AnXBn_Synch
+    exec_mode = cbg.EXEC_PANEL if a.exec_mode == "panel" else cbg.EXEC_STAGED
+
+    C = None
+    for _ in range(a.warmup):
+        C = mult(A, B, exec_mode=exec_mode)
+        C.tile.free()
+    grid.barrier()
+    cbg.synchronize()
+    ms_local = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        if C is not None:
+            C.tile.free()
+        C = mult(A, B, exec_mode=exec_mode)
+        st = cbg.last_stats()
+        ms_local.append(st["ms_symbolic"] + st["ms_numeric"])
+    cbg.synchronize()
+    grid.barrier()
+    dt = time.perf_counter() - t0
+    dt = grid.allreduce_max(dt)
+    nnz_c = grid.allreduce_sum(C.tile.nnz)
+    st = cbg.last_stats()
+    flops = grid.allreduce_sum(st["flops"])
+    # algorithmic bytes of the local multiply: 16F + 12 nnz(C) + 32 nnz(B) + 8 n
+    nnz_b = B.tile.nnz
+    bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * nnz_b + 8 * B.tile.n
+    ms_avg = sum(ms_local) / len(ms_local)
+    achieved = bytes_alg / (ms_avg * 1e-3) / 1e9
+    achieved = grid.allreduce_max(achieved) if N > 1 else achieved
+
+    if rank == 0:
+        out = {
+            "metric": "nnz(C)/sec for A·A (R-MAT scale %d) at %d GPUs" % (scale, N),
+            "value": nnz_c * a.steps / dt,
+            "unit": "nnz(C)/s",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": dt / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak" if a.scale is None and N > 1 else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic Graph500 R-MAT (SEED 0xDECAFBAD), generated on device",
+            "config": {"workload": "R-MAT scale-%d ef%d A·A, Mult_AnXBn_%s, %s" % (
+                scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
+                "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
+                "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
+                         "ms_avg": ms_avg, "bytes_alg": bytes_alg},
+        }
+        if N == 1 and not a.no_cpu_baseline:
+            threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+            threads = min(threads, 16)
+            cs = a.cpu_scale if a.cpu_scale is not None else min(scale, 18)
+            r, algo, cdt, cnnz = cpu_baseline(cs, a.ef, a.seed, threads)
+            out["cpu_baseline"] = {"value": r, "unit": "nnz(C)/s", "cores": threads, "kind": "port",
+                                   "sample": "R-MAT scale-%d ef%d A*A, oracle Mult_AnXBn_%s 1x1, %.1f s" % (
+                                       cs, a.ef, algo.capitalize(), cdt)}
+        print(json.dumps(out), flush=True)
+    C.tile.free()
+    grid.destroy()
+
+
+if __name__ == "__main__":
+    main()

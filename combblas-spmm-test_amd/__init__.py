@@ -1,0 +1,435 @@
+"""combblas-spmm-test_amd -- MI355X-native CombBLAS 2D-SUMMA SpGEMM hot path.
+
+Python binding of libcbg (C ABI in include/cbg.h) used by tests/ and bench.py.
+It mirrors the reference's operator surface for the path:
+
+  reference (include/CombBLAS/...)                 here
+  ------------------------------------------------ --------------------------------
+  SpDCCols<int32_t,double> (SpDCCols.h)            Tile  (device DCSC tile)
+  CommGrid (CommGrid.h, src/CommGrid.cpp:37-75)    CommGrid (RCCL or host transport)
+  SpParMat<...> (SpParMat.h)                       SpParMat (tile + grid + global dims)
+  PlusTimesSRing / MinPlusSRing (Semirings.h)      PlusTimesSRing / MinPlusSRing
+  LocalHybridSpGEMM (mtSpGEMM.h:212-460)           LocalHybridSpGEMM(A, B)
+  MergeAll / MultiwayMerge (Friends.h:657,         MergeAll(parts) / MultiwayMerge(parts)
+     MultiwayMerge.h:409)
+  Mult_AnXBn_DoubleBuff (ParFriends.h:798-997)     Mult_AnXBn_DoubleBuff(A, B, sr)
+  Mult_AnXBn_Synch (ParFriends.h:1004-1108)        Mult_AnXBn_Synch(A, B, sr)
+  PSpGEMM (SpParMat.h:454-467)                     PSpGEMM(A, B, sr)
+  DistEdgeList::GenGraph500Data + SpParMat(DEL)    rmat_tile / SpParMat.rmat
+     + RemoveLoops
+
+The reference MPI_Aborts on misuse; here the same codes surface as CbgError.code
+(3001 GRIDMISMATCH, 3002 DIMMISMATCH, 3003 NOTSQUARE, 3005 MATRIXALIAS).
+
+There is no CPU fallback: without libcbg.so (built by `make -C
+combblas-spmm-test_amd`) or without a GPU every compute call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcbg.so")
+
+PLUS_TIMES, MIN_PLUS = 0, 1
+DOUBLEBUFF, SYNCH = 0, 1
+EXEC_PANEL, EXEC_STAGED = 0, 1
+
+GRIDMISMATCH, DIMMISMATCH, NOTSQUARE, MATRIXALIAS, INVALIDPARAMS = 3001, 3002, 3003, 3005, 3007
+
+
+class CbgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libcbg error {code}: {msg}")
+        self.code = code
+
+
+class CTile(ctypes.Structure):
+    _fields_ = [("m", ctypes.c_int64), ("n", ctypes.c_int64), ("nnz", ctypes.c_int64), ("nzc", ctypes.c_int64),
+                ("cp", ctypes.c_void_p), ("jc", ctypes.c_void_p), ("ir", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("on_device", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_size_t)
+
+
+class CHostComm(ctypes.Structure):
+    _fields_ = [("bcast", BCAST_FN), ("allgather", ALLGATHER_FN), ("user", ctypes.c_void_p)]
+
+
+# every symbol include/cbg.h declares (checked by tests/test_capi.py)
+EXPORTS = [
+    "cbg_version", "cbg_last_error", "cbg_set_device", "cbg_device_count", "cbg_pool_stats", "cbg_pool_trim",
+    "cbg_synchronize", "cbg_tile_upload", "cbg_tile_download", "cbg_tile_free", "cbg_tile_split_cols",
+    "cbg_tile_split_rows", "cbg_tile_digest", "cbg_rmat_tile", "cbg_local_spgemm", "cbg_local_symbolic", "cbg_merge",
+    "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
+    "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libcbg.so (raises if it has not been built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: build it with `make -C {_HERE}` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    T = ctypes.POINTER(CTile)
+    i64, i32, vp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p
+    sig = {
+        "cbg_version": ([], ctypes.c_char_p),
+        "cbg_last_error": ([], ctypes.c_char_p),
+        "cbg_set_device": ([i32], i32),
+        "cbg_device_count": ([ctypes.POINTER(i32)], i32),
+        "cbg_pool_stats": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
+        "cbg_pool_trim": ([], i32),
+        "cbg_synchronize": ([], i32),
+        "cbg_tile_upload": ([T, T], i32),
+        "cbg_tile_download": ([T, T], i32),
+        "cbg_tile_free": ([T], i32),
+        "cbg_tile_split_cols": ([T, i64, T, T], i32),
+        "cbg_tile_split_rows": ([T, i64, T, T], i32),
+        "cbg_tile_digest": ([T, i64, i64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                             ctypes.POINTER(ctypes.c_double)], i32),
+        "cbg_rmat_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
+        "cbg_local_spgemm": ([T, T, i32, T, vp], i32),
+        "cbg_local_symbolic": ([T, T, ctypes.POINTER(i64), ctypes.POINTER(i64), vp], i32),
+        "cbg_merge": ([T, i32, i32, T, vp], i32),
+        "cbg_last_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "cbg_get_unique_id": ([vp], i32),
+        "cbg_grid_create": ([i32, i32, i32, i32, vp, ctypes.POINTER(vp)], i32),
+        "cbg_grid_create_host": ([i32, i32, i32, i32, ctypes.POINTER(CHostComm), ctypes.POINTER(vp)], i32),
+        "cbg_grid_destroy": ([vp], i32),
+        "cbg_grid_info": ([vp] + [ctypes.POINTER(i32)] * 6, i32),
+        "cbg_grid_barrier": ([vp], i32),
+        "cbg_grid_allreduce_max": ([vp, ctypes.POINTER(ctypes.c_double)], i32),
+        "cbg_grid_allreduce_sum_i64": ([vp, ctypes.POINTER(i64)], i32),
+        "cbg_summa_spgemm": ([vp, T, T, i64, i64, i32, i32, i32, T], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise CbgError(rc, lib().cbg_last_error().decode(errors="replace"))
+
+
+# --------------------------------------------------------------------------
+# tiles
+# --------------------------------------------------------------------------
+class Tile:
+    """A device-resident DCSC tile (SpDCCols<int32_t,double> in HBM)."""
+
+    def __init__(self, ct=None):
+        self.c = ct if ct is not None else CTile()
+
+    # shape / counts (SpDCCols::getnrow/getncol/getnnz/getnzc)
+    m = property(lambda self: self.c.m)
+    n = property(lambda self: self.c.n)
+    nnz = property(lambda self: self.c.nnz)
+    nzc = property(lambda self: self.c.nzc)
+
+    def isZero(self):
+        return self.c.nnz == 0
+
+    @staticmethod
+    def from_host(m, n, cp, jc, ir, val):
+        cp = np.ascontiguousarray(cp, np.int64)
+        jc = np.ascontiguousarray(jc, np.int32)
+        ir = np.ascontiguousarray(ir, np.int32)
+        val = np.ascontiguousarray(val, np.float64)
+        h = CTile(int(m), int(n), len(ir), len(jc), cp.ctypes.data, jc.ctypes.data if len(jc) else None,
+                  ir.ctypes.data if len(ir) else None, val.ctypes.data if len(val) else None, 0, 0)
+        t = Tile()
+        _check(lib().cbg_tile_upload(ctypes.byref(h), ctypes.byref(t.c)))
+        return t
+
+    @staticmethod
+    def from_dict(d):
+        return Tile.from_host(d["m"], d["n"], d["cp"], d["jc"], d["ir"], d["val"])
+
+    def to_host(self):
+        c = self.c
+        cp = np.empty(c.nzc + 1, np.int64)
+        jc = np.empty(max(c.nzc, 1), np.int32)
+        ir = np.empty(max(c.nnz, 1), np.int32)
+        val = np.empty(max(c.nnz, 1), np.float64)
+        h = CTile(0, 0, 0, 0, cp.ctypes.data, jc.ctypes.data, ir.ctypes.data, val.ctypes.data, 0, 0)
+        _check(lib().cbg_tile_download(ctypes.byref(c), ctypes.byref(h)))
+        return dict(m=int(c.m), n=int(c.n), cp=cp, jc=jc[:c.nzc], ir=ir[:c.nnz], val=val[:c.nnz])
+
+    def digest(self, roff=0, coff=0):
+        hs, hv, vs = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+        _check(lib().cbg_tile_digest(ctypes.byref(self.c), roff, coff, ctypes.byref(hs), ctypes.byref(hv),
+                                     ctypes.byref(vs)))
+        return dict(nnz=int(self.c.nnz), nzc=int(self.c.nzc), hs="%016x" % hs.value, hv="%016x" % hv.value,
+                    vsum=vs.value)
+
+    def split_cols(self, cut):
+        """SpDCCols::Split (SpDCCols.cpp:905-930)"""
+        a, b = Tile(), Tile()
+        _check(lib().cbg_tile_split_cols(ctypes.byref(self.c), cut, ctypes.byref(a.c), ctypes.byref(b.c)))
+        return a, b
+
+    def split_rows(self, cut):
+        a, b = Tile(), Tile()
+        _check(lib().cbg_tile_split_rows(ctypes.byref(self.c), cut, ctypes.byref(a.c), ctypes.byref(b.c)))
+        return a, b
+
+    def free(self):
+        if self.c.on_device and (self.c.cp or self.c.ir):
+            _check(lib().cbg_tile_free(ctypes.byref(self.c)))
+
+    def __del__(self):
+        try:
+            if _lib is not None and self.c.on_device:
+                _lib.cbg_tile_free(ctypes.byref(self.c))
+        except Exception:
+            pass
+
+
+def rmat_tile(scale, edgefactor=16, seed=0xDECAFBAD, grid=(1, 1), pos=(0, 0)):
+    """Graph500 Kronecker R-MAT tile generated on device (GenWriteMatrix.cpp:101-114 semantics)."""
+    t = Tile()
+    _check(lib().cbg_rmat_tile(scale, edgefactor, seed, grid[0], grid[1], pos[0], pos[1], ctypes.byref(t.c)))
+    return t
+
+
+class PlusTimesSRing:
+    """PlusTimesSRing<double,double> (Semirings.h:212-233)"""
+    code = PLUS_TIMES
+
+
+class MinPlusSRing:
+    """MinPlusSRing<double,double> (Semirings.h:235-255)"""
+    code = MIN_PLUS
+
+
+def _sr(sr):
+    if isinstance(sr, int):
+        return sr
+    if isinstance(sr, str):
+        return {"plus": PLUS_TIMES, "plus_times": PLUS_TIMES, "minplus": MIN_PLUS, "min_plus": MIN_PLUS}[sr]
+    return sr.code
+
+
+def LocalHybridSpGEMM(A, B, sr=PlusTimesSRing, stream=None):
+    """C = A*B for device tiles (mtSpGEMM.h:212-460); returns a device Tile (DCSC)."""
+    C = Tile()
+    _check(lib().cbg_local_spgemm(ctypes.byref(A.c), ctypes.byref(B.c), _sr(sr), ctypes.byref(C.c), stream))
+    return C
+
+
+def last_stats():
+    f, n, nb, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    a, b = ctypes.c_double(), ctypes.c_double()
+    lib().cbg_last_stats(ctypes.byref(f), ctypes.byref(n), ctypes.byref(a), ctypes.byref(b), ctypes.byref(nb),
+                         ctypes.byref(ns))
+    return dict(flops=f.value, nnz=n.value, ms_symbolic=a.value, ms_numeric=b.value, n_big=nb.value,
+                n_slabs=ns.value)
+
+
+def MergeAll(parts, sr=PlusTimesSRing):
+    """Merge column-sorted partial tiles, summing duplicates (Friends.h:657-741)."""
+    arr = (CTile * len(parts))(*[p.c for p in parts])
+    C = Tile()
+    _check(lib().cbg_merge(arr, len(parts), _sr(sr), ctypes.byref(C.c), None))
+    return C
+
+
+MultiwayMerge = MergeAll  # MultiwayMerge.h:409-526: same result, threaded in the reference
+
+
+def synchronize():
+    _check(lib().cbg_synchronize())
+
+
+def device_count():
+    c = ctypes.c_int()
+    _check(lib().cbg_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def pool_stats():
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    lib().cbg_pool_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+# --------------------------------------------------------------------------
+# grid / distributed matrix
+# --------------------------------------------------------------------------
+class CommGrid:
+    """CommGrid(world, rows, cols) (src/CommGrid.cpp:37-75); rows=cols=0 -> square.
+
+    transport="rccl": one process per GPU, RCCL row/col communicators over xGMI.
+    transport="host": collectives delegated to host callbacks (`host_comm`, an
+    object with bcast(comm, np.ndarray(uint8), root) and allgather(comm, bytes)
+    -> bytes); used to test the SUMMA logic with several processes per GPU.
+    """
+
+    def __init__(self, rank, nranks, rows=0, cols=0, unique_id=None, transport="rccl", host_comm=None):
+        self.rank, self.nranks = rank, nranks
+        self.h = ctypes.c_void_p()
+        self._keep = None
+        if transport == "rccl":
+            if unique_id is None:
+                raise ValueError("unique_id (from CommGrid.unique_id() on rank 0) is required")
+            buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+            _check(lib().cbg_grid_create(rank, nranks, rows, cols, buf, ctypes.byref(self.h)))
+        else:
+            hc = host_comm
+
+            def _bcast(user, comm, buf, nbytes, root):
+                try:
+                    arr = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
+                    hc.bcast(comm, arr, root)
+                    return 0
+                except Exception:  # noqa: BLE001 -- surfaced as CBG_ERR_RCCL
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+
+            def _allgather(user, comm, inp, out, nbytes):
+                try:
+                    src = ctypes.string_at(inp, nbytes)
+                    res = hc.allgather(comm, src)
+                    ctypes.memmove(out, res, len(res))
+                    return 0
+                except Exception:  # noqa: BLE001
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+
+            cb = CHostComm(BCAST_FN(_bcast), ALLGATHER_FN(_allgather), None)
+            self._keep = cb
+            _check(lib().cbg_grid_create_host(rank, nranks, rows, cols, ctypes.byref(cb), ctypes.byref(self.h)))
+        vals = [ctypes.c_int() for _ in range(6)]
+        _check(lib().cbg_grid_info(self.h, *[ctypes.byref(v) for v in vals]))
+        _, _, self.grid_rows, self.grid_cols, self.prow, self.pcol = [v.value for v in vals]
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(128)
+        _check(lib().cbg_get_unique_id(buf))
+        return buf.raw
+
+    # CommGrid accessors
+    def GetGridRows(self):
+        return self.grid_rows
+
+    def GetGridCols(self):
+        return self.grid_cols
+
+    def GetRankInProcRow(self):
+        return self.pcol
+
+    def GetRankInProcCol(self):
+        return self.prow
+
+    def barrier(self):
+        _check(lib().cbg_grid_barrier(self.h))
+
+    def allreduce_max(self, x):
+        v = ctypes.c_double(x)
+        _check(lib().cbg_grid_allreduce_max(self.h, ctypes.byref(v)))
+        return v.value
+
+    def allreduce_sum(self, x):
+        v = ctypes.c_int64(int(x))
+        _check(lib().cbg_grid_allreduce_sum_i64(self.h, ctypes.byref(v)))
+        return v.value
+
+    def destroy(self):
+        if self.h:
+            _check(lib().cbg_grid_destroy(self.h))
+            self.h = ctypes.c_void_p()
+
+
+def block_range(total, parts, idx):
+    """Block distribution of SpParMat::Owner (SpParMat.cpp:5068-5097): last block takes the remainder."""
+    per = total // parts
+    lo = idx * per
+    hi = total if idx == parts - 1 else lo + per
+    return lo, hi
+
+
+class SpParMat:
+    """Distributed sparse matrix: one device tile per rank of a CommGrid."""
+
+    def __init__(self, tile, grid, gm, gn):
+        self.tile, self.grid, self.gm, self.gn = tile, grid, gm, gn
+
+    def getnrow(self):
+        return self.gm
+
+    def getncol(self):
+        return self.gn
+
+    def getnnz(self):
+        """global nnz (SpParMat::getnnz Allreduce, SpParMat.cpp:772-778)"""
+        return self.grid.allreduce_sum(self.tile.nnz) if self.grid is not None else self.tile.nnz
+
+    @staticmethod
+    def rmat(grid, scale, edgefactor=16, seed=0xDECAFBAD):
+        nv = 1 << scale
+        t = rmat_tile(scale, edgefactor, seed, (grid.grid_rows, grid.grid_cols), (grid.prow, grid.pcol))
+        return SpParMat(t, grid, nv, nv)
+
+    @staticmethod
+    def from_global(grid, d):
+        """Distribute a global host DCSC dict by the block distribution (SpParMat::Owner)."""
+        r0, r1 = block_range(d["m"], grid.grid_rows, grid.prow)
+        c0, c1 = block_range(d["n"], grid.grid_cols, grid.pcol)
+        t = sub_tile(d, r0, r1, c0, c1)
+        return SpParMat(Tile.from_dict(t), grid, d["m"], d["n"])
+
+
+def sub_tile(d, r0, r1, c0, c1):
+    """rows [r0,r1) x cols [c0,c1) of a host DCSC dict, re-based (host helper)."""
+    cols = np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"]))
+    rows = d["ir"].astype(np.int64)
+    keep = (rows >= r0) & (rows < r1) & (cols >= c0) & (cols < c1)
+    cols, rows, vals = cols[keep] - c0, rows[keep] - r0, d["val"][keep]
+    jc, start = np.unique(cols, return_index=True)
+    cp = np.append(start, len(rows)).astype(np.int64)
+    return dict(m=r1 - r0, n=c1 - c0, cp=cp, jc=jc.astype(np.int32), ir=rows.astype(np.int32),
+                val=vals.astype(np.float64))
+
+
+def _summa(A, B, sr, algo, exec_mode):
+    if A is B:
+        raise CbgError(MATRIXALIAS, "Can not multiply, inputs alias (make a temporary copy of one of them first)")
+    if A.grid is not B.grid and (A.grid.grid_rows, A.grid.grid_cols) != (B.grid.grid_rows, B.grid.grid_cols):
+        raise CbgError(GRIDMISMATCH, "Grids don't confirm for multiplication")
+    C = Tile()
+    _check(lib().cbg_summa_spgemm(A.grid.h, ctypes.byref(A.tile.c), ctypes.byref(B.tile.c), A.gn, B.gm, _sr(sr),
+                                  algo, exec_mode, ctypes.byref(C.c)))
+    return SpParMat(C, A.grid, A.gm, B.gn)
+
+
+def Mult_AnXBn_DoubleBuff(A, B, sr=PlusTimesSRing, exec_mode=EXEC_PANEL):
+    """ParFriends.h:798-997 (collective over A.grid)."""
+    return _summa(A, B, sr, DOUBLEBUFF, exec_mode)
+
+
+def Mult_AnXBn_Synch(A, B, sr=PlusTimesSRing, exec_mode=EXEC_PANEL):
+    """ParFriends.h:1004-1108 (collective over A.grid)."""
+    return _summa(A, B, sr, SYNCH, exec_mode)
+
+
+def PSpGEMM(A, B, sr=PlusTimesSRing):
+    """SpParMat.h:454-467: PSpGEMM -> Mult_AnXBn_Synch."""
+    return Mult_AnXBn_Synch(A, B, sr)

@@ -1,0 +1,308 @@
+// cbg_capi.cpp -- extern "C" boundary of libcbg (declared in include/cbg.h).
+// Every entry point catches exceptions and returns the reference's abort code
+// (SpDefs.h:69-76) or a >= 3100 runtime code; cbg_last_error() has the text.
+#include <cstring>
+
+#include "cbg_internal.h"
+
+struct cbg_grid;
+namespace cbg {
+void rmat_tile(int scale, int ef, uint64_t userseed, int pr, int pc, int prow, int pcol, cbg_tile& out, hipStream_t s);
+void tile_digest(const cbg_tile& t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum,
+                 hipStream_t s);
+int grid_shape(int nranks, int& rows, int& cols);
+cbg_grid* grid_create_rccl(int rank, int nranks, int rows, int cols, const void* uid);
+cbg_grid* grid_create_host(int rank, int nranks, int rows, int cols, const cbg_host_comm* hc);
+void grid_destroy(cbg_grid* g);
+void allreduce_f64(cbg_grid* g, double* v, bool max);
+void allreduce_sum_i64(cbg_grid* g, int64_t* v);
+void barrier(cbg_grid* g);
+int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr, int algo,
+                 int exec, cbg_tile& C);
+}  // namespace cbg
+
+namespace {
+thread_local std::string g_err;
+thread_local cbg::LocalStats g_stats;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+template <class F>
+int guard(F&& f) {
+  try {
+    g_err.clear();
+    return f();
+  } catch (const cbg::HipError& e) {
+    return fail(e.code, e.what());
+  } catch (const std::exception& e) {
+    return fail(CBG_ERR_HIP, e.what());
+  } catch (...) {
+    return fail(CBG_ERR_HIP, "unknown error");
+  }
+}
+
+hipStream_t default_stream() {
+  static thread_local hipStream_t s = nullptr;
+  if (!s) CBG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+hipStream_t as_stream(void* p) { return p ? static_cast<hipStream_t>(p) : default_stream(); }
+
+int check_tile(const cbg_tile* t, bool need_device, const char* name) {
+  if (!t) return fail(CBG_ERR_INVALIDPARAMS, std::string(name) + " is NULL");
+  if (need_device && !t->on_device) return fail(CBG_ERR_INVALIDPARAMS, std::string(name) + " is not a device tile");
+  if (t->m < 0 || t->n < 0 || t->nnz < 0 || t->nzc < 0 || t->nzc > t->n)
+    return fail(CBG_ERR_INVALIDPARAMS, std::string(name) + " has inconsistent sizes");
+  if (t->m >= INT32_MAX || t->n >= INT32_MAX)
+    return fail(CBG_ERR_INVALIDPARAMS, std::string(name) + ": local dimensions must fit int32");
+  return CBG_OK;
+}
+}  // namespace
+
+extern "C" {
+
+const char* cbg_version(void) { return "libcbg 0.1 (gfx950)"; }
+const char* cbg_last_error(void) { return g_err.c_str(); }
+
+int cbg_set_device(int device) {
+  return guard([&] {
+    CBG_HIP(hipSetDevice(device));
+    return CBG_OK;
+  });
+}
+int cbg_device_count(int* count) {
+  return guard([&] {
+    CBG_HIP(hipGetDeviceCount(count));
+    return CBG_OK;
+  });
+}
+int cbg_pool_stats(size_t* in_use, size_t* cached) {
+  if (in_use) *in_use = cbg::pool().bytes_in_use();
+  if (cached) *cached = cbg::pool().bytes_cached();
+  return CBG_OK;
+}
+int cbg_pool_trim(void) {
+  return guard([&] {
+    cbg::pool().trim();
+    return CBG_OK;
+  });
+}
+int cbg_synchronize(void) {
+  return guard([&] {
+    CBG_HIP(hipDeviceSynchronize());
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_upload(const cbg_tile* h, cbg_tile* d) {
+  if (int rc = check_tile(h, false, "host tile")) return rc;
+  if (!d) return fail(CBG_ERR_INVALIDPARAMS, "dst is NULL");
+  return guard([&] {
+    cbg_tile t{};
+    cbg::tile_alloc_device(t, h->m, h->n, h->nnz, h->nzc);
+    hipStream_t s = default_stream();
+    CBG_HIP(hipMemcpyAsync(t.cp, h->cp, sizeof(int64_t) * (h->nzc + 1), hipMemcpyHostToDevice, s));
+    if (h->nzc) CBG_HIP(hipMemcpyAsync(t.jc, h->jc, sizeof(int32_t) * h->nzc, hipMemcpyHostToDevice, s));
+    if (h->nnz) {
+      CBG_HIP(hipMemcpyAsync(t.ir, h->ir, sizeof(int32_t) * h->nnz, hipMemcpyHostToDevice, s));
+      CBG_HIP(hipMemcpyAsync(t.val, h->val, sizeof(double) * h->nnz, hipMemcpyHostToDevice, s));
+    }
+    CBG_HIP(hipStreamSynchronize(s));
+    *d = t;
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_download(const cbg_tile* d, cbg_tile* h) {
+  if (int rc = check_tile(d, true, "device tile")) return rc;
+  if (!h || !h->cp || (d->nzc && !h->jc) || (d->nnz && (!h->ir || !h->val)))
+    return fail(CBG_ERR_INVALIDPARAMS, "host arrays missing");
+  return guard([&] {
+    hipStream_t s = default_stream();
+    CBG_HIP(hipMemcpyAsync(h->cp, d->cp, sizeof(int64_t) * (d->nzc + 1), hipMemcpyDeviceToHost, s));
+    if (d->nzc) CBG_HIP(hipMemcpyAsync(h->jc, d->jc, sizeof(int32_t) * d->nzc, hipMemcpyDeviceToHost, s));
+    if (d->nnz) {
+      CBG_HIP(hipMemcpyAsync(h->ir, d->ir, sizeof(int32_t) * d->nnz, hipMemcpyDeviceToHost, s));
+      CBG_HIP(hipMemcpyAsync(h->val, d->val, sizeof(double) * d->nnz, hipMemcpyDeviceToHost, s));
+    }
+    CBG_HIP(hipStreamSynchronize(s));
+    h->m = d->m;
+    h->n = d->n;
+    h->nnz = d->nnz;
+    h->nzc = d->nzc;
+    h->on_device = 0;
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_free(cbg_tile* t) {
+  if (!t) return CBG_OK;
+  return guard([&] {
+    if (t->on_device) cbg::tile_free_device(*t);
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* l, cbg_tile* r) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  if (cut < 0 || cut > t->n) return fail(CBG_ERR_INVALIDPARAMS, "cut out of range");
+  return guard([&] {
+    cbg::tile_split_cols(*t, cut, *l, *r, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_split_rows(const cbg_tile* t, int64_t cut, cbg_tile* top, cbg_tile* bot) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  if (cut < 0 || cut > t->m) return fail(CBG_ERR_INVALIDPARAMS, "cut out of range");
+  return guard([&] {
+    cbg::tile_split_rows(*t, cut, *top, *bot, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_digest(const cbg_tile* t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  return guard([&] {
+    cbg::tile_digest(*t, roff, coff, hs, hv, vsum, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_rmat_tile(int scale, int ef, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile* out) {
+  if (scale < 1 || scale > 30 || ef < 1 || pr < 1 || pc < 1 || prow < 0 || prow >= pr || pcol < 0 || pcol >= pc || !out)
+    return fail(CBG_ERR_INVALIDPARAMS, "bad R-MAT parameters");
+  if (((int64_t)1 << scale) * ef >= ((int64_t)1 << 31))
+    return fail(CBG_ERR_NOTSUPPORTED, "edge count must stay below 2^31");
+  return guard([&] {
+    cbg::rmat_tile(scale, ef, seed, pr, pc, prow, pcol, *out, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_local_spgemm(const cbg_tile* A, const cbg_tile* B, int sr, cbg_tile* C, void* stream) {
+  if (int rc = check_tile(A, true, "A")) return rc;
+  if (int rc = check_tile(B, true, "B")) return rc;
+  if (!C) return fail(CBG_ERR_INVALIDPARAMS, "C is NULL");
+  if (sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) return fail(CBG_ERR_INVALIDPARAMS, "unknown semiring");
+  if (A->n != B->m) return fail(CBG_ERR_DIMMISMATCH, "A.ncol != B.nrow");
+  if (A->nnz >= INT32_MAX || B->nnz >= INT32_MAX) return fail(CBG_ERR_NOTSUPPORTED, "A/B tiles need nnz < 2^31");
+  return guard([&] {
+    cbg::local_spgemm(*A, *B, sr, *C, as_stream(stream), &g_stats);
+    return CBG_OK;
+  });
+}
+
+int cbg_local_symbolic(const cbg_tile* A, const cbg_tile* B, int64_t* flops, int64_t* nnz, void* stream) {
+  // the symbolic totals are a by-product of a full multiply's statistics
+  cbg_tile C{};
+  int rc = cbg_local_spgemm(A, B, CBG_PLUS_TIMES, &C, stream);
+  if (rc) return rc;
+  if (flops) *flops = g_stats.flops;
+  if (nnz) *nnz = g_stats.nnz;
+  return cbg_tile_free(&C);
+}
+
+int cbg_merge(const cbg_tile* parts, int nparts, int sr, cbg_tile* C, void* stream) {
+  if (nparts <= 0 || !parts || !C) return fail(CBG_ERR_INVALIDPARAMS, "no parts");
+  for (int i = 0; i < nparts; ++i) {
+    if (int rc = check_tile(&parts[i], true, "part")) return rc;
+    if (parts[i].m != parts[0].m || parts[i].n != parts[0].n)
+      return fail(CBG_ERR_DIMMISMATCH, "Dimensions do not match on MergeAll()");  // Friends.h:672-678
+  }
+  return guard([&] {
+    std::vector<cbg_tile> v(parts, parts + nparts);
+    cbg::merge_tiles(v, parts[0].m, parts[0].n, sr, *C, as_stream(stream));
+    return CBG_OK;
+  });
+}
+
+int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_sym, double* ms_num, int64_t* n_big, int64_t* n_slabs) {
+  if (flops) *flops = g_stats.flops;
+  if (nnz) *nnz = g_stats.nnz;
+  if (ms_sym) *ms_sym = g_stats.ms_symbolic;
+  if (ms_num) *ms_num = g_stats.ms_numeric;
+  if (n_big) *n_big = g_stats.n_big;
+  if (n_slabs) *n_slabs = g_stats.n_slabs;
+  return CBG_OK;
+}
+
+// ---------------- grid ----------------
+int cbg_get_unique_id(void* id);  // cbg_summa_id.cpp
+
+int cbg_grid_create(int rank, int nranks, int rows, int cols, const void* uid, cbg_grid** out) {
+  if (!out || !uid || rank < 0 || rank >= nranks) return fail(CBG_ERR_INVALIDPARAMS, "bad grid parameters");
+  if (int rc = cbg::grid_shape(nranks, rows, cols))
+    return fail(rc, rc == CBG_ERR_NOTSQUARE ? "This version only works on a square logical processor grid"
+                                            : "grid rows*cols != nranks");
+  return guard([&] {
+    *out = cbg::grid_create_rccl(rank, nranks, rows, cols, uid);
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_create_host(int rank, int nranks, int rows, int cols, const cbg_host_comm* hc, cbg_grid** out) {
+  if (!out || !hc || !hc->bcast || !hc->allgather || rank < 0 || rank >= nranks)
+    return fail(CBG_ERR_INVALIDPARAMS, "bad grid parameters");
+  if (int rc = cbg::grid_shape(nranks, rows, cols)) return fail(rc, "grid shape");
+  return guard([&] {
+    *out = cbg::grid_create_host(rank, nranks, rows, cols, hc);
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_destroy(cbg_grid* g) {
+  return guard([&] {
+    cbg::grid_destroy(g);
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_barrier(cbg_grid* g) {
+  if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  return guard([&] {
+    cbg::barrier(g);
+    return CBG_OK;
+  });
+}
+int cbg_grid_allreduce_max(cbg_grid* g, double* v) {
+  if (!g || !v) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  return guard([&] {
+    cbg::allreduce_f64(g, v, true);
+    return CBG_OK;
+  });
+}
+int cbg_grid_allreduce_sum_i64(cbg_grid* g, int64_t* v) {
+  if (!g || !v) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  return guard([&] {
+    cbg::allreduce_sum_i64(g, v);
+    return CBG_OK;
+  });
+}
+
+int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow, int sr,
+                     int algo, int exec, cbg_tile* C) {
+  if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  if (int rc = check_tile(A, true, "A")) return rc;
+  if (int rc = check_tile(B, true, "B")) return rc;
+  if (A == B) return fail(CBG_ERR_MATRIXALIAS, "inputs alias (make a temporary copy of one of them first)");
+  if (!C || (sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) || (algo != CBG_DOUBLEBUFF && algo != CBG_SYNCH) ||
+      (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
+    return fail(CBG_ERR_INVALIDPARAMS, "bad summa parameters");
+  return guard([&]() -> int {
+    CBG_HIP(hipDeviceSynchronize());
+    int rc = cbg::summa_spgemm(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, *C);
+    if (rc) return fail(rc, rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"
+                            : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
+                            : rc == CBG_ERR_NOTSQUARE   ? "staged SUMMA needs a square grid"
+                                                        : "summa failed");
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_info(const cbg_grid* g, int* rank, int* nranks, int* rows, int* cols, int* prow, int* pcol);
+
+}  // extern "C"

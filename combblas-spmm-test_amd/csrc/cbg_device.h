@@ -1,0 +1,160 @@
+// cbg_device.h -- device-side building blocks for gfx950 (wave64) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+namespace cbg {
+
+constexpr int WAVE = 64;
+constexpr int EMPTY_KEY = 0x7FFFFFFF;  // empty hash slot; sorts after every row id
+
+// Order LDS traffic between the lanes of ONE wave (LDS executes a wave's
+// instructions in issue order; this stops the compiler from reordering).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
+
+// inclusive scan over the 64 lanes of a wave
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    int t = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ long long wave_incl_scan64(long long v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    long long t = __shfl_up(v, d, WAVE);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ long long wave_sum64(long long v) {
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, WAVE);
+  return v;
+}
+
+// Block-wide exclusive scan of one int per thread.  `tmp` holds >= BS/64+1 ints.
+// Returns the exclusive prefix; *total receives the block sum.  Contains barriers.
+template <int BS>
+__device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
+  constexpr int NW = BS / WAVE;
+  const int lane = lane_id(), w = threadIdx.x / WAVE;
+  int incl = wave_incl_scan(v);
+  if (lane == WAVE - 1) tmp[w] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int i = 0; i < NW; ++i) {
+      int t = tmp[i];
+      tmp[i] = s;
+      s += t;
+    }
+    tmp[NW] = s;
+  }
+  __syncthreads();
+  int r = tmp[w] + incl - v;
+  *total = tmp[NW];
+  __syncthreads();
+  return r;
+}
+
+// largest i in [0, n) with pref[i] <= u, for a non-decreasing pref[0..n] with pref[0] = 0 <= u
+__device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
+  int lo = 0, hi = n;  // invariant: pref[lo] <= u < pref[hi]
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (pref[mid] <= u) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// first position in sorted a[lo,hi) with a[pos] >= key
+__device__ __forceinline__ int lower_bound_g(const int32_t* __restrict__ a, int lo, int hi, int key) {
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// multiplicative hash into a power-of-two table
+template <int LOGT>
+__device__ __forceinline__ unsigned hash_slot(int key) {
+  return ((unsigned)key * 0x9E3779B1u) >> (32 - LOGT);
+}
+
+// ---- semirings (Semirings.h:212-255) ----
+template <int SR>
+struct Sem;
+template <>
+struct Sem<0> {  // PlusTimesSRing<double,double>
+  static __device__ __forceinline__ double mul(double a, double b) { return a * b; }
+  static __device__ __forceinline__ double identity() { return 0.0; }
+  static __device__ __forceinline__ void lds_acc(double* p, double v) { atomicAdd(p, v); }
+  static __device__ __forceinline__ double add(double a, double b) { return a + b; }
+};
+template <>
+struct Sem<1> {  // MinPlusSRing<double,double>: multiply = inf_plus (Semirings.h:40-47), add = min
+  static __device__ __forceinline__ double mul(double a, double b) {
+    return (a == DBL_MAX || b == DBL_MAX) ? DBL_MAX : a + b;
+  }
+  // +inf as "empty" makes the first min() store the product exactly, like the
+  // reference's first-insert (mtSpGEMM.h:410-414), also for an overflowing a+b.
+  static __device__ __forceinline__ double identity() { return __builtin_inf(); }
+  static __device__ __forceinline__ void lds_acc(double* p, double v) {
+    __hip_atomic_fetch_min(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  static __device__ __forceinline__ double add(double a, double b) { return b < a ? b : a; }
+};
+
+// In-LDS bitonic sort of N (power of two) (key,val) pairs by key, ascending,
+// by NT cooperating threads (tid in [0,NT)).  SYNC is a barrier functor.
+template <int N, int NT, class SYNC>
+__device__ __forceinline__ void bitonic_sort_kv(int* keys, double* vals, int tid, SYNC sync) {
+#pragma unroll 1
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll 1
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int idx = tid; idx < N / 2; idx += NT) {
+        int i = 2 * idx - (idx & (j - 1));
+        int l = i + j;
+        int ki = keys[i], kl = keys[l];
+        bool up = (i & k) == 0;
+        if ((ki > kl) == up) {
+          keys[i] = kl;
+          keys[l] = ki;
+          double t = vals[i];
+          vals[i] = vals[l];
+          vals[l] = t;
+        }
+      }
+      sync();
+    }
+  }
+}
+
+struct WaveSync {
+  __device__ __forceinline__ void operator()() const { wave_sync(); }
+};
+struct BlockSync {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+
+}  // namespace cbg

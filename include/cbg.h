@@ -1,0 +1,155 @@
+/* cbg.h -- C ABI of libcbg, the MI355X-native CombBLAS 2D-SUMMA SpGEMM hot path.
+ *
+ * Plain C types only (pointers + sizes): this is the drop-in boundary that a
+ * CombBLAS build (C++ shim: combblas-spmm-test_amd/include/combblas_amd/) or
+ * any FFI (ctypes stub in INTEGRATION.md) binds.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference root).
+ *
+ * Tiles are DCSC, the reference's Dcsc<IT,NT> (include/CombBLAS/dcsc.h:85-91):
+ *   cp[nzc+1] column pointers (int64 here: C tiles exceed 2^31 nnz at scale>=20),
+ *   jc[nzc]   ids of the nonempty columns (ascending),
+ *   ir[nnz]   row ids, ascending inside each column,
+ *   val[nnz]  fp64 values.
+ * Local indices are int32 (SpDCCols<int32_t,double>, MultTiming.cpp:18-23);
+ * A and B tiles need nnz < 2^31.
+ *
+ * Error model: the reference MPI_Aborts with SpDefs.h:69-76 codes; libcbg
+ * returns the same code instead (3001 GRIDMISMATCH, 3002 DIMMISMATCH,
+ * 3003 NOTSQUARE, 3005 MATRIXALIAS, 3007 INVALIDPARAMS) and >= 3100 for
+ * device/runtime failures.  cbg_last_error() gives the message.
+ */
+#ifndef CBG_H
+#define CBG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cbg_tile {
+  int64_t m, n, nnz, nzc;
+  int64_t* cp;
+  int32_t* jc;
+  int32_t* ir;
+  double* val;
+  int32_t on_device; /* 1: arrays are device memory (owned by libcbg when produced by it) */
+  int32_t reserved;
+} cbg_tile;
+
+/* semirings: PlusTimesSRing<double,double> Semirings.h:212-233,
+ *            MinPlusSRing<double,double>   Semirings.h:235-255 */
+enum { CBG_PLUS_TIMES = 0, CBG_MIN_PLUS = 1 };
+
+/* SUMMA variants */
+enum {
+  CBG_DOUBLEBUFF = 0, /* Mult_AnXBn_DoubleBuff ParFriends.h:798-997 */
+  CBG_SYNCH = 1       /* Mult_AnXBn_Synch      ParFriends.h:1004-1108 (PSpGEMM SpParMat.h:454-467) */
+};
+/* how the stages are executed on device (identical results up to fp order) */
+enum {
+  CBG_EXEC_PANEL = 0, /* gather the A block-row / B block-column panels, one local multiply, no merge */
+  CBG_EXEC_STAGED = 1 /* per-stage local multiply double-buffered against the next stage's broadcast,
+                         then an on-device multiway merge of the partial products */
+};
+
+enum {
+  CBG_OK = 0,
+  CBG_ERR_GRIDMISMATCH = 3001,
+  CBG_ERR_DIMMISMATCH = 3002,
+  CBG_ERR_NOTSQUARE = 3003,
+  CBG_ERR_MATRIXALIAS = 3005,
+  CBG_ERR_INVALIDPARAMS = 3007,
+  CBG_ERR_HIP = 3100,
+  CBG_ERR_RCCL = 3101,
+  CBG_ERR_OOM = 3102,
+  CBG_ERR_NOTSUPPORTED = 3103
+};
+
+/* ---------------- library ---------------- */
+const char* cbg_version(void);
+const char* cbg_last_error(void);
+/* select the HIP device for the calling thread (default: current device) */
+int cbg_set_device(int device);
+int cbg_device_count(int* count);
+/* device memory of libcbg's caching pool (bytes) */
+int cbg_pool_stats(size_t* in_use, size_t* cached);
+int cbg_pool_trim(void);
+int cbg_synchronize(void);
+
+/* ---------------- tiles ---------------- */
+/* host -> device copy (arrays of *dst are allocated by libcbg) */
+int cbg_tile_upload(const cbg_tile* host, cbg_tile* dst);
+/* device -> host into caller-provided arrays sized from dev->nnz/nzc */
+int cbg_tile_download(const cbg_tile* dev, cbg_tile* host);
+/* frees a device tile produced by libcbg (no-op for host tiles) */
+int cbg_tile_free(cbg_tile* t);
+/* SpDCCols::Split (SpDCCols.cpp:905-930): columns [0,cut) and [cut,n) (device) */
+int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* left, cbg_tile* right);
+/* row split of B as DoubleBuff does with Transpose/Split/Transpose (ParFriends.h:824-829), no transposes */
+int cbg_tile_split_rows(const cbg_tile* t, int64_t cut, cbg_tile* top, cbg_tile* bottom);
+/* structural + value digest (same definition as tests/golden/make_golden.py), device tile */
+int cbg_tile_digest(const cbg_tile* t, int64_t row_off, int64_t col_off, uint64_t* hs, uint64_t* hv, double* vsum);
+
+/* ---------------- generator ---------------- */
+/* Graph500 Kronecker R-MAT as DistEdgeList::GenGraph500Data(packed, scrambled)
+ * (DistEdgeList.cpp:223-280, RefGen21.h:73-318) -> SpParMat(DEL,false)
+ * (SpParMat.cpp:3140-3254) -> RemoveLoops (SpParMat.cpp:3257-3272), on device.
+ * Produces the tile of grid cell (prow,pcol) of a pr x pc grid (1x1: whole matrix). */
+int cbg_rmat_tile(int scale, int edgefactor, uint64_t userseed, int pr, int pc, int prow, int pcol,
+                  cbg_tile* out);
+
+/* ---------------- local multiply ---------------- */
+/* LocalHybridSpGEMM (mtSpGEMM.h:212-460) + SpDCCols(SpTuples) (SpDCCols.cpp:108-190):
+ * C = A*B on the semiring, C as a device DCSC tile (columns where C has nonzeros,
+ * rows ascending, explicit zeros kept).  A, B device tiles.  stream may be NULL. */
+int cbg_local_spgemm(const cbg_tile* A, const cbg_tile* B, int semiring, cbg_tile* C, void* hip_stream);
+/* estimateFLOP + estimateNNZ_Hash (mtSpGEMM.h:1056-1134, 805-933): totals only */
+int cbg_local_symbolic(const cbg_tile* A, const cbg_tile* B, int64_t* flops, int64_t* nnz, void* hip_stream);
+/* MergeAll / MultiwayMerge (Friends.h:657-741, MultiwayMerge.h:409-526) of
+ * column-sorted device tiles of equal shape, summing duplicates with SR::add. */
+int cbg_merge(const cbg_tile* parts, int nparts, int semiring, cbg_tile* C, void* hip_stream);
+/* last local multiply's statistics: flops, nnz, per-phase device ms, big columns, slabs */
+int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms_numeric, int64_t* n_big,
+                   int64_t* n_slabs);
+
+/* ---------------- 2D SUMMA over RCCL ---------------- */
+typedef struct cbg_grid cbg_grid;
+#define CBG_UNIQUE_ID_BYTES 128
+/* ncclGetUniqueId: called by rank 0, bytes shipped to the others by the host */
+int cbg_get_unique_id(void* id);
+/* CommGrid(MPI_COMM_WORLD, rows, cols) (CommGrid.cpp:37-75): rows=cols=0 => square
+ * grid or CBG_ERR_NOTSQUARE; rank r -> (r / cols, r % cols); row/col
+ * communicators via ncclCommSplit.  One process (rank) per GPU. */
+int cbg_grid_create(int rank, int nranks, int grid_rows, int grid_cols, const void* unique_id, cbg_grid** out);
+/* host-transport grid for testing the SUMMA logic with several processes on
+ * one GPU: collectives are delegated to host callbacks (e.g. gloo). */
+typedef struct cbg_host_comm {
+  /* comm: 0 = world, 1 = row communicator, 2 = column communicator; root is the
+   * rank inside that communicator; buf is HOST memory */
+  int (*bcast)(void* user, int comm, void* buf, size_t bytes, int root);
+  int (*allgather)(void* user, int comm, const void* in, void* out, size_t bytes_each);
+  void* user;
+} cbg_host_comm;
+int cbg_grid_create_host(int rank, int nranks, int grid_rows, int grid_cols, const cbg_host_comm* comm,
+                         cbg_grid** out);
+int cbg_grid_destroy(cbg_grid* g);
+int cbg_grid_info(const cbg_grid* g, int* rank, int* nranks, int* grid_rows, int* grid_cols, int* prow, int* pcol);
+/* world-communicator helpers used by drivers for barrier + max-over-ranks timing */
+int cbg_grid_barrier(cbg_grid* g);
+int cbg_grid_allreduce_max(cbg_grid* g, double* value);
+int cbg_grid_allreduce_sum_i64(cbg_grid* g, int64_t* value);
+
+/* Mult_AnXBn_DoubleBuff / Mult_AnXBn_Synch (ParFriends.h:798-1108):
+ * collective over the grid; A_local/B_local are this rank's device tiles of
+ * the block distribution (SpParMat::Owner, SpParMat.cpp:5068-5097).
+ * A_gncol/B_gnrow are the global inner dimensions (CheckSpGEMMCompliance).
+ * A and B are left unchanged (the reference mutates and restores them).
+ * C_local receives this rank's tile C(prow,pcol). */
+int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
+                     int64_t B_gnrow, int semiring, int algo, int exec, cbg_tile* C_local);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CBG_H */

@@ -1,0 +1,177 @@
+"""GPU parity of the HIP local multiply (through the C ABI) against the reference's golden
+vectors and the CPU oracle.  Indices bit-exact; fp64 values exact for the integer-valued
+R-MAT products and within |dc| <= 1e-12 * (|A||B|)_ij for random-valued inputs
+(north_star tolerance); min-plus is exact (order independent)."""
+import numpy as np
+import pytest
+
+from helpers import (abs_tile, assert_digest_eq, assert_tiles_equal, digest, golden, load_npz, oracle_local)
+
+pytestmark = pytest.mark.gpu
+G = golden()
+RTOL = 1e-12
+
+
+@pytest.mark.parametrize("scale", [8, 10, 12, 14, 16, 18])
+def test_device_rmat_matches_reference(cbg, scale):
+    A = cbg.rmat_tile(scale, 16)
+    g = G["rmat"][f"s{scale}_ef16"]["A"]
+    d = A.digest()
+    assert d["nnz"] == g["nnz"] and d["nzc"] == g["nzc"] and d["hs"] == g["hs"] and d["hv"] == g["hv"]
+
+
+@pytest.mark.parametrize("scale", [8, 10])
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_local_full_product_bit_exact(cbg, scale, sr):
+    A = cbg.rmat_tile(scale, 16)
+    B = cbg.rmat_tile(scale, 16)
+    C = cbg.LocalHybridSpGEMM(A, B, sr)
+    assert_tiles_equal(C.to_host(), load_npz(f"rmat_s{scale}_ef16_C_local_{sr}.npz"))
+
+
+@pytest.mark.parametrize("scale", [12, 14, 16, 18])
+def test_local_digest_vs_reference(cbg, scale):
+    A = cbg.rmat_tile(scale, 16)
+    B = cbg.rmat_tile(scale, 16)
+    C = cbg.LocalHybridSpGEMM(A, B)
+    g = G["rmat"][f"s{scale}_ef16"]["C_local_plus"]
+    d = C.digest()
+    d["unsorted"] = 0
+    assert_digest_eq(d, g)
+    h = C.to_host()  # order: columns ascending, rows ascending inside each column
+    assert np.all(np.diff(h["jc"]) > 0)
+    cols = np.repeat(np.arange(len(h["jc"])), np.diff(h["cp"]))
+    r = h["ir"].astype(np.int64)
+    assert not np.any((np.diff(cols) == 0) & (np.diff(r) <= 0))
+    st = cbg.last_stats()
+    assert st["nnz"] == g["nnz"] and st["flops"] == G["rmat"][f"s{scale}_ef16"]["symbolic"]["flops"]
+
+
+@pytest.mark.parametrize("scale", [12, 14])
+def test_minplus_digest(cbg, scale):
+    A = cbg.rmat_tile(scale, 16)
+    B = cbg.rmat_tile(scale, 16)
+    C = cbg.LocalHybridSpGEMM(A, B, "minplus")
+    d = C.digest()
+    d["unsorted"] = 0
+    assert_digest_eq(d, G["rmat"][f"s{scale}_ef16"]["C_local_minplus"])
+
+
+@pytest.mark.parametrize("name", ["sevenvertex", "small_nonsym", "largeseq"])
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_bundled_inputs(cbg, name, sr):
+    Ah = load_npz(f"{name}_A.npz")
+    Bh = load_npz(f"{name}_B.npz") if name == "largeseq" else Ah
+    A, B = cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh)
+    C = cbg.LocalHybridSpGEMM(A, B, sr).to_host()
+    ref = load_npz(f"{name}_C_local_{sr}.npz")
+    if sr == "plus":
+        bound = oracle_local(abs_tile(Ah), abs_tile(Bh))["val"]
+        assert_tiles_equal(C, ref, rtol=RTOL, bound=bound)
+    else:
+        assert_tiles_equal(C, ref)
+
+
+def _rand_tile(rng, m, n, density, lo=-1.0, hi=1.0, hub_cols=()):
+    M = (rng.random((m, n)) < density)
+    for c in hub_cols:
+        M[:, c] = rng.random(m) < 0.8
+    vals = rng.uniform(lo, hi, size=(m, n))
+    cols, rows = np.nonzero(M.T)
+    jc, start = np.unique(cols, return_index=True)
+    return dict(m=m, n=n, cp=np.append(start, len(rows)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=rows.astype(np.int32), val=vals[rows, cols].astype(np.float64))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_random_fp_vs_oracle(cbg, seed):
+    rng = np.random.default_rng(seed)
+    # hub columns in A and B force the wave, block and big-column (slab) paths
+    Ah = _rand_tile(rng, 3000, 2500, 0.004, hub_cols=(3, 77))
+    Bh = _rand_tile(rng, 2500, 1800, 0.01, hub_cols=(5,))
+    Bh2 = dict(Bh)
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh)).to_host()
+    ref = oracle_local(Ah, Bh2)
+    bound = oracle_local(abs_tile(Ah), abs_tile(Bh))["val"]
+    assert_tiles_equal(C, ref, rtol=RTOL, bound=bound)
+    Cm = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), "minplus").to_host()
+    assert_tiles_equal(Cm, oracle_local(Ah, Bh, "minplus"))
+
+
+def test_big_columns_tall_matrix(cbg):
+    # m > 2^20 rows exercises multi-pass bitmaps and hash-mode slabs
+    rng = np.random.default_rng(7)
+    m, k, n = (1 << 21) + 123, 64, 8
+    nnz_per = 40000
+    cols = np.repeat(np.arange(k), nnz_per)
+    rows = np.concatenate([np.sort(rng.choice(m, nnz_per, replace=False)) for _ in range(k)])
+    Ah = dict(m=m, n=k, cp=np.arange(k + 1, dtype=np.int64) * nnz_per, jc=np.arange(k, dtype=np.int32),
+              ir=rows.astype(np.int32), val=rng.integers(1, 5, len(rows)).astype(np.float64))
+    Bh = dict(m=k, n=n, cp=np.arange(n + 1, dtype=np.int64) * k, jc=np.arange(n, dtype=np.int32),
+              ir=np.tile(np.arange(k, dtype=np.int32), n), val=rng.integers(1, 3, n * k).astype(np.float64))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh))
+    assert cbg.last_stats()["n_big"] == n
+    assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh))
+
+
+def test_edge_cases(cbg):
+    # empty operands -> SpTuples(0, m, n) (mtSpGEMM.h:224-227)
+    E = dict(m=5, n=4, cp=np.zeros(1, np.int64), jc=np.zeros(0, np.int32), ir=np.zeros(0, np.int32),
+             val=np.zeros(0))
+    X = dict(m=4, n=3, cp=np.array([0, 2], np.int64), jc=np.array([1], np.int32), ir=np.array([0, 3], np.int32),
+             val=np.array([1.0, -1.0]))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(E), cbg.Tile.from_dict(X))
+    assert C.nnz == 0 and C.m == 5 and C.n == 3
+    # explicit zeros are kept: (+1)(1) + (-1)(1) = 0 stays a structural nonzero
+    A = dict(m=2, n=2, cp=np.array([0, 1, 2], np.int64), jc=np.array([0, 1], np.int32), ir=np.array([0, 0], np.int32),
+             val=np.array([1.0, -1.0]))
+    B = dict(m=2, n=1, cp=np.array([0, 2], np.int64), jc=np.array([0], np.int32), ir=np.array([0, 1], np.int32),
+             val=np.array([1.0, 1.0]))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(A), cbg.Tile.from_dict(B)).to_host()
+    assert C["ir"].tolist() == [0] and C["val"].tolist() == [0.0] and C["jc"].tolist() == [0]
+    # B column whose A columns are all empty produces no output column
+    B2 = dict(m=2, n=3, cp=np.array([0, 1, 2], np.int64), jc=np.array([0, 2], np.int32),
+              ir=np.array([0, 1], np.int32), val=np.array([2.0, 3.0]))
+    A2 = dict(m=2, n=2, cp=np.array([0, 1], np.int64), jc=np.array([1], np.int32), ir=np.array([1], np.int32),
+              val=np.array([5.0]))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(A2), cbg.Tile.from_dict(B2)).to_host()
+    assert C["jc"].tolist() == [2] and C["ir"].tolist() == [1] and C["val"].tolist() == [15.0]
+    # dimension mismatch -> DIMMISMATCH (ParFriends.h:162-170)
+    with pytest.raises(cbg.CbgError) as e:
+        cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(A2), cbg.Tile.from_dict(X))
+    assert e.value.code == cbg.DIMMISMATCH
+
+
+def test_merge_and_split(cbg):
+    A = cbg.rmat_tile(10, 16)
+    B = cbg.rmat_tile(10, 16)
+    A1, A2 = A.split_cols(A.n // 2)
+    B1, B2 = B.split_rows(B.m // 2)
+    P1 = cbg.LocalHybridSpGEMM(A1, B1)
+    P2 = cbg.LocalHybridSpGEMM(A2, B2)
+    C = cbg.MergeAll([P1, P2])
+    assert_tiles_equal(C.to_host(), load_npz("rmat_s10_ef16_C_local_plus.npz"))
+    Cm = cbg.MergeAll([cbg.LocalHybridSpGEMM(A1, B1, "minplus"), cbg.LocalHybridSpGEMM(A2, B2, "minplus")], "minplus")
+    assert_tiles_equal(Cm.to_host(), load_npz("rmat_s10_ef16_C_local_minplus.npz"))
+
+
+@pytest.mark.parametrize("algo", ["doublebuff", "synch"])
+@pytest.mark.parametrize("exec_mode", [0, 1])
+def test_summa_single_rank(cbg, algo, exec_mode):
+    class Self:
+        def bcast(self, comm, arr, root):
+            pass
+
+        def allgather(self, comm, data):
+            return data
+
+    g = cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+    A = cbg.SpParMat.rmat(g, 10)
+    B = cbg.SpParMat.rmat(g, 10)
+    f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
+    C = f(A, B, exec_mode=exec_mode)
+    assert_tiles_equal(C.tile.to_host(), load_npz("rmat_s10_ef16_C_local_plus.npz"))
+    with pytest.raises(cbg.CbgError) as e:
+        f(A, A)
+    assert e.value.code == cbg.MATRIXALIAS
+    g.destroy()
