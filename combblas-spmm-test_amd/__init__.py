@@ -358,6 +358,48 @@ class CommGrid:
             self.h = ctypes.c_void_p()
 
 
+class GlooHostComm:
+    """Host transport for CommGrid(transport="host") over torch.distributed (gloo).
+
+    Builds one process group per grid row and per grid column (ranks ascending,
+    so the rank inside a row group is the grid column and inside a column group
+    the grid row, as CommGrid's MPI_Comm_split keys give, src/CommGrid.cpp:66-67).
+    Used to run the SUMMA logic with several processes on one GPU and in CPU tests.
+    """
+
+    def __init__(self, grid_rows, grid_cols):
+        import torch  # noqa: F401
+        import torch.distributed as dist
+        self.dist = dist
+        self.pr, self.pc = grid_rows, grid_cols
+        self.rank = dist.get_rank()
+        self.prow, self.pcol = self.rank // grid_cols, self.rank % grid_cols
+        self.rows = [dist.new_group([r * grid_cols + c for c in range(grid_cols)]) for r in range(grid_rows)]
+        self.cols = [dist.new_group([r * grid_cols + c for r in range(grid_rows)]) for c in range(grid_cols)]
+
+    def _group(self, comm):
+        if comm == 1:
+            return self.rows[self.prow], lambda root: self.prow * self.pc + root
+        if comm == 2:
+            return self.cols[self.pcol], lambda root: root * self.pc + self.pcol
+        return None, lambda root: root
+
+    def bcast(self, comm, arr, root):
+        import torch
+        g, glob = self._group(comm)
+        t = torch.from_numpy(arr)
+        self.dist.broadcast(t, src=glob(root), group=g)
+
+    def allgather(self, comm, data):
+        import torch
+        g, _ = self._group(comm)
+        size = self.dist.get_world_size(g) if g is not None else self.dist.get_world_size()
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(size)]
+        self.dist.all_gather(out, t, group=g)
+        return b"".join(o.numpy().tobytes() for o in out)
+
+
 def block_range(total, parts, idx):
     """Block distribution of SpParMat::Owner (SpParMat.cpp:5068-5097): last block takes the remainder."""
     per = total // parts

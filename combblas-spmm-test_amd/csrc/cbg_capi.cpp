@@ -23,7 +23,6 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 
 namespace {
 thread_local std::string g_err;
-thread_local cbg::LocalStats g_stats;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -191,7 +190,8 @@ int cbg_local_spgemm(const cbg_tile* A, const cbg_tile* B, int sr, cbg_tile* C, 
   if (A->n != B->m) return fail(CBG_ERR_DIMMISMATCH, "A.ncol != B.nrow");
   if (A->nnz >= INT32_MAX || B->nnz >= INT32_MAX) return fail(CBG_ERR_NOTSUPPORTED, "A/B tiles need nnz < 2^31");
   return guard([&] {
-    cbg::local_spgemm(*A, *B, sr, *C, as_stream(stream), &g_stats);
+    cbg::thread_stats() = cbg::LocalStats{};
+    cbg::local_spgemm(*A, *B, sr, *C, as_stream(stream));
     return CBG_OK;
   });
 }
@@ -201,8 +201,8 @@ int cbg_local_symbolic(const cbg_tile* A, const cbg_tile* B, int64_t* flops, int
   cbg_tile C{};
   int rc = cbg_local_spgemm(A, B, CBG_PLUS_TIMES, &C, stream);
   if (rc) return rc;
-  if (flops) *flops = g_stats.flops;
-  if (nnz) *nnz = g_stats.nnz;
+  if (flops) *flops = cbg::thread_stats().flops;
+  if (nnz) *nnz = cbg::thread_stats().nnz;
   return cbg_tile_free(&C);
 }
 
@@ -214,6 +214,7 @@ int cbg_merge(const cbg_tile* parts, int nparts, int sr, cbg_tile* C, void* stre
       return fail(CBG_ERR_DIMMISMATCH, "Dimensions do not match on MergeAll()");  // Friends.h:672-678
   }
   return guard([&] {
+    cbg::thread_stats() = cbg::LocalStats{};
     std::vector<cbg_tile> v(parts, parts + nparts);
     cbg::merge_tiles(v, parts[0].m, parts[0].n, sr, *C, as_stream(stream));
     return CBG_OK;
@@ -221,6 +222,7 @@ int cbg_merge(const cbg_tile* parts, int nparts, int sr, cbg_tile* C, void* stre
 }
 
 int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_sym, double* ms_num, int64_t* n_big, int64_t* n_slabs) {
+  const cbg::LocalStats& g_stats = cbg::thread_stats();
   if (flops) *flops = g_stats.flops;
   if (nnz) *nnz = g_stats.nnz;
   if (ms_sym) *ms_sym = g_stats.ms_symbolic;
@@ -293,6 +295,7 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t 
       (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
     return fail(CBG_ERR_INVALIDPARAMS, "bad summa parameters");
   return guard([&]() -> int {
+    cbg::thread_stats() = cbg::LocalStats{};
     CBG_HIP(hipDeviceSynchronize());
     int rc = cbg::summa_spgemm(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, *C);
     if (rc) return fail(rc, rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"

@@ -84,8 +84,11 @@ struct LocalStats {
   int64_t n_big = 0, n_slabs = 0;
   double ms_symbolic = 0, ms_numeric = 0;
 };
+// Every call accumulates into the calling thread's stats (reset by the C ABI
+// at the start of each public entry point); `st` optionally receives this call's.
 void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s,
                   LocalStats* st = nullptr);
+LocalStats& thread_stats();
 
 // device exclusive scan of n int64 values -> out[0..n], returns nothing (total at out[n])
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);

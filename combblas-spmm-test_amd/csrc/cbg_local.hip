@@ -603,6 +603,7 @@ __global__ void k_col_scatter(int64_t n, const int32_t* __restrict__ cnt, const 
 // ----------------------------------------------------------------------------
 // host orchestration
 // ----------------------------------------------------------------------------
+void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st);
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 template <class K>
@@ -707,7 +708,25 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
 }
 
+LocalStats& thread_stats() {
+  static thread_local LocalStats t;
+  return t;
+}
+
 void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st) {
+  LocalStats mine;
+  local_spgemm_impl(A, B, semiring, C, s, &mine);
+  LocalStats& t = thread_stats();
+  t.flops += mine.flops;
+  t.nnz += mine.nnz;
+  t.n_big += mine.n_big;
+  t.n_slabs += mine.n_slabs;
+  t.ms_symbolic += mine.ms_symbolic;
+  t.ms_numeric += mine.ms_numeric;
+  if (st) *st = mine;
+}
+
+void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st) {
   C = cbg_tile{};
   C.m = A.m;
   C.n = B.n;

@@ -1,0 +1,117 @@
+"""Worker for multi-process SUMMA tests (launched by torch.distributed.run).
+
+usage: mp_worker.py <mode> <grid_rows> <grid_cols> <case>
+  mode "gpu": every rank runs the HIP SUMMA over the host (gloo) transport on the
+              shared GPU and checks the global digest against the reference's.
+  mode "cpu": transport plumbing only (no device work): bcast/allgather through
+              GlooHostComm and the block distribution of the golden matrix.
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from conftest import load_cbg  # noqa: E402
+from helpers import digest, golden, load_npz  # noqa: E402
+
+
+def add_digests(ds):
+    hs = sum(int(d["hs"], 16) for d in ds) % (1 << 64)
+    hv = sum(int(d["hv"], 16) for d in ds) % (1 << 64)
+    return dict(nnz=sum(d["nnz"] for d in ds), hs="%016x" % hs, hv="%016x" % hv, vsum=sum(d["vsum"] for d in ds))
+
+
+def main():
+    mode, pr, pc, case = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    cbg = load_cbg()
+    if mode == "gpu":
+        cbg.lib()
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    assert world == pr * pc
+    hc = cbg.GlooHostComm(pr, pc)
+    G = golden()
+    if case.startswith("rmat"):
+        A = load_npz("rmat_s10_ef16_A.npz")
+        B = A
+        gd = G["rmat"]["s10_ef16"]["C_local_plus"]
+    else:
+        A = load_npz("largeseq_A.npz")
+        B = load_npz("largeseq_B.npz")
+        gd = G["files"]["largeseq"]["C_local_plus"]
+    if mode == "cpu":
+        # tiles of the block distribution cover A exactly once
+        r0, r1 = cbg.block_range(A["m"], pr, hc.prow)
+        c0, c1 = cbg.block_range(A["n"], pc, hc.pcol)
+        t = cbg.sub_tile(A, r0, r1, c0, c1)
+        d = digest(t, r0, c0)
+        import pickle
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(d))))]
+        tot = add_digests(alld)
+        ga = G["rmat"]["s10_ef16"]["A"] if case.startswith("rmat") else G["files"]["largeseq"]["A"]
+        assert tot["nnz"] == ga["nnz"] and tot["hs"] == ga["hs"] and tot["hv"] == ga["hv"], (tot, ga)
+        # row / column broadcasts reach exactly the grid row / column
+        buf = np.full(16, 255, np.uint8)
+        if hc.pcol == 0:
+            buf[:] = hc.prow
+        hc.bcast(1, buf, 0)
+        assert np.all(buf == hc.prow)
+        buf[:] = 255
+        if hc.prow == pr - 1:
+            buf[:] = 100 + hc.pcol
+        hc.bcast(2, buf, pr - 1)
+        assert np.all(buf == 100 + hc.pcol)
+        got = hc.allgather(1, bytes([hc.rank]))
+        assert list(got) == [hc.prow * pc + c for c in range(pc)]
+        got = hc.allgather(2, bytes([hc.rank]))
+        assert list(got) == [r * pc + hc.pcol for r in range(pr)]
+        dist.barrier()
+        if rank == 0:
+            print("MPOK", flush=True)
+        return
+    grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+    Ad = cbg.SpParMat.from_global(grid, A)
+    Bd = cbg.SpParMat.from_global(grid, B)
+    ok = True
+    for algo in ("doublebuff", "synch"):
+        for ex in ((0, 1) if pr == pc else (0,)):
+            f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
+            C = f(Ad, Bd, exec_mode=ex)
+            r0, _ = cbg.block_range(A["m"], pr, grid.prow)
+            c0, _ = cbg.block_range(B["n"], pc, grid.pcol)
+            d = C.tile.digest(r0, c0)
+            import pickle
+            alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(d))))]
+            tot = add_digests(alld)
+            good = tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"]
+            if case.startswith("rmat"):
+                good = good and tot["hv"] == gd["hv"]
+            else:
+                good = good and abs(tot["vsum"] - gd["vsum"]) < 1e-9 * max(1, abs(gd["vsum"]))
+            if rank == 0:
+                print(algo, ex, "OK" if good else f"BAD {tot} vs {gd}", flush=True)
+            ok = ok and good
+            C.tile.free()
+    grid.destroy()
+    dist.barrier()
+    if rank == 0 and ok:
+        print("MPOK", flush=True)
+
+
+PAD = 512
+
+
+def _pad(b):
+    assert len(b) <= PAD
+    return b + b" " * (PAD - len(b))
+
+
+def _chunks(b):
+    return [b[i:i + PAD].rstrip(b" ") for i in range(0, len(b), PAD)]
+
+
+if __name__ == "__main__":
+    main()
