@@ -159,7 +159,8 @@ def main():
             "config": {"workload": "R-MAT scale-%d ef%d A·A, Mult_AnXBn_%s, %s" % (
                 scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
-                "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3)},
+                "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
+                "big_columns": st["n_big"], "slabs": st["n_slabs"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",

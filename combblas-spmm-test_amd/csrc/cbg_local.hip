@@ -207,9 +207,10 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
 // ----------------------------------------------------------------------------
 // symbolic for big columns: LDS bitmap over row passes + slab plan
 // ----------------------------------------------------------------------------
-constexpr int FINE_LOG = 14;          // fine row range = 16384 rows = 512 bitmap words
-constexpr int SLAB_HASH_CAP = 4096;   // max nnz of a hash-mode slab (table 8192)
-constexpr int SLAB_DENSE_MIN = 1024;  // a fine range with >= this many nnz becomes a dense slab
+constexpr int FINE_LOG = 13;            // fine row range = 8192 rows = 256 bitmap words
+constexpr int SLAB_CAP = 12288;         // max nnz of a slab (LDS value array, 96 KiB)
+constexpr int SLAB_SPAN_LOG = 18;       // max rows of a slab (LDS bitmap, 32 KiB)
+constexpr int SLAB_WORDS = 1 << (SLAB_SPAN_LOG - 5);
 constexpr int BIG_BS = 1024;
 
 __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
@@ -272,7 +273,8 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
     __syncthreads();
   }
   if (tid == 0) {
-    // greedy slab plan over fine ranges
+    // greedy slab plan over fine ranges: consecutive ranges while the slab
+    // holds <= SLAB_CAP nonzeros and spans <= 2^SLAB_SPAN_LOG rows
     int total = 0, ns = 0, off = 0;
     int g_lo = -1, g_hi = 0, g_cnt = 0;
     int4* d = desc + (int64_t)b * nfine;
@@ -282,17 +284,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
       if (c == 0) continue;
       const int lo = f << FINE_LOG;
       const int hi = (int)min((int64_t)(f + 1) << FINE_LOG, m);
-      if (c >= SLAB_DENSE_MIN) {
-        if (g_cnt) {
-          d[ns++] = make_int4(g_lo, g_hi, off, g_cnt);
-          off += g_cnt;
-          g_cnt = 0;
-        }
-        d[ns++] = make_int4(lo, hi, off, c | (1 << 30));
-        off += c;
-        continue;
-      }
-      if (g_cnt + c > SLAB_HASH_CAP) {
+      if (g_cnt && (g_cnt + c > SLAB_CAP || hi - g_lo > (1 << SLAB_SPAN_LOG))) {
         d[ns++] = make_int4(g_lo, g_hi, off, g_cnt);
         off += g_cnt;
         g_cnt = 0;
@@ -464,14 +456,34 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
   }
 }
 
-// numeric: one row slab of a big column (dense LDS accumulator or LDS hash)
-constexpr int SLAB_BS = 1024;
-constexpr int SLAB_DENSE_ROWS = 1 << FINE_LOG;
-constexpr int SLAB_LOGT = 13;
-constexpr int SLAB_UNION_BYTES = (SLAB_DENSE_ROWS * 8 + (SLAB_DENSE_ROWS / 32) * 4) > ((1 << SLAB_LOGT) * 12)
-                                     ? (SLAB_DENSE_ROWS * 8 + (SLAB_DENSE_ROWS / 32) * 4)
-                                     : ((1 << SLAB_LOGT) * 12);
-constexpr int SLAB_LDS_BYTES = SLAB_UNION_BYTES + SLAB_BS * 8 + (SLAB_BS + 4) * 4 + SLAB_BS * 4 + (SLAB_BS / WAVE + 4) * 4;
+// numeric: one row slab of a big column by bitmap + rank.
+// Pass 1 marks the slab's rows in an LDS bitmap, a scan turns the bitmap into
+// ranks (= output positions, rows ascending), pass 2 accumulates each product
+// into the LDS value slot of its rank.  No hashing, no sort, coalesced output.
+constexpr int SLAB_BS = 512;
+constexpr int SLAB_LDS_BYTES = SLAB_CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + SLAB_BS * 8 + (SLAB_BS + 4) * 4 +
+                               SLAB_BS * 4 + (SLAB_BS / WAVE + 4) * 4;
+static_assert(SLAB_LDS_BYTES <= 160 * 1024, "slab LDS");
+
+template <int SR>
+__device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
+                                              const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                              int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
+  constexpr int BS = SLAB_BS;
+  for (int u = threadIdx.x; u < total; u += BS) {
+    const int sg = seg_search(pref, BS, u);
+    const int q = st[sg] + (u - pref[sg]);
+    const int r = irA[q] - lo;
+    const int w = r >> 5;
+    const unsigned bit = 1u << (r & 31);
+    if (pass == 0) {
+      atomicOr(&bm[w], bit);
+    } else {
+      const int pos = wpre[w] + __popc(bm[w] & (bit - 1u));
+      Sem<SR>::lds_acc(&vals[pos], Sem<SR>::mul(valA[q], bv[sg]));
+    }
+  }
+}
 
 template <int SR>
 __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
@@ -482,104 +494,90 @@ __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ l
                                                       const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
   constexpr int BS = SLAB_BS;
-  constexpr int T = 1 << SLAB_LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* acc = reinterpret_cast<double*>(smem);                  // dense: [16384] / hash: vals[8192]
-  unsigned* bm = reinterpret_cast<unsigned*>(acc + SLAB_DENSE_ROWS);  // dense bitmap [512]
-  int* keys = reinterpret_cast<int*>(acc + T);                   // hash keys [8192]
-  double* bv = reinterpret_cast<double*>(smem + SLAB_UNION_BYTES);
-  int* pref = reinterpret_cast<int*>(bv + BS);
-  int* st = pref + BS + 4;
-  int* tmp = st + BS;
+  double* vals = reinterpret_cast<double*>(smem);                          // [SLAB_CAP]
+  double* bv = vals + SLAB_CAP;                                            // [BS]
+  unsigned* bm = reinterpret_cast<unsigned*>(bv + BS);                     // [SLAB_WORDS]
+  int* pref = reinterpret_cast<int*>(bm + SLAB_WORDS);                     // [BS+1]
+  int* st = pref + BS + 4;                                                 // [BS]
+  int* tmp = st + BS;                                                      // scan scratch
+  unsigned short* wpre = reinterpret_cast<unsigned short*>(tmp + BS / WAVE + 4);  // [SLAB_WORDS]
   const int tid = threadIdx.x;
   const int2 e = list[blockIdx.x];
   const int4 d = desc[(int64_t)e.x * nfine + e.y];
   const int col = perm_big[e.x];
-  const bool dense = (d.w >> 30) & 1;
-  const int nout = d.w & ((1 << 30) - 1);
+  const int nout = d.w;
   const int lo = d.x, hi = d.y;
+  const int words = (hi - lo + 31) >> 5;
   const int64_t obase = colptr[col] + d.z;
-  if (dense) {
-    for (int j = tid; j < SLAB_DENSE_ROWS; j += BS) acc[j] = Sem<SR>::identity();
-    for (int j = tid; j < SLAB_DENSE_ROWS / 32; j += BS) bm[j] = 0u;
-  } else {
-    for (int j = tid; j < T; j += BS) {
-      keys[j] = EMPTY_KEY;
-      acc[j] = Sem<SR>::identity();
-    }
-  }
+  for (int j = tid; j < words; j += BS) bm[j] = 0u;
+  for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
   __syncthreads();
-  const int64_t p1 = cpB[col + 1];
-  for (int64_t c0 = cpB[col]; c0 < p1; c0 += BS) {
-    const int64_t p = c0 + tid;
-    int s = 0, len = 0;
-    double bval = 0.0;
-    if (p < p1) {
-      int2 ce = cmap[irB[p]];
-      if (ce.y > 0) {
-        const int a = lower_bound_g(irA, ce.x, ce.x + ce.y, lo);
-        const int z = lower_bound_g(irA, a, ce.x + ce.y, hi);
-        s = a;
-        len = z - a;
-      }
-      bval = valB[p];
-    }
-    int total;
-    const int ex = block_excl_scan<BS>(len, tmp, &total);
-    pref[tid] = ex;
-    if (tid == BS - 1) pref[BS] = total;
-    st[tid] = s;
-    bv[tid] = bval;
-    __syncthreads();
-    if (dense) {
-      for (int u = tid; u < total; u += BS) {
-        const int sg = seg_search(pref, BS, u);
-        const int q = st[sg] + (u - pref[sg]);
-        const int r = irA[q] - lo;
-        Sem<SR>::lds_acc(&acc[r], Sem<SR>::mul(valA[q], bv[sg]));
-        atomicOr(&bm[r >> 5], 1u << (r & 31));
-      }
-    } else {
-      for (int u = tid; u < total; u += BS) {
-        const int sg = seg_search(pref, BS, u);
-        const int q = st[sg] + (u - pref[sg]);
-        const int row = irA[q];
-        const double v = Sem<SR>::mul(valA[q], bv[sg]);
-        unsigned h = hash_slot<SLAB_LOGT>(row);
-        while (true) {
-          const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-          if (old == EMPTY_KEY || old == row) {
-            Sem<SR>::lds_acc(&acc[h], v);
-            break;
+  const int64_t p0 = cpB[col], p1 = cpB[col + 1];
+  const bool one_chunk = (p1 - p0) <= BS;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int64_t c0 = p0; c0 < p1; c0 += BS) {
+      int total;
+      if (pass == 0 || !one_chunk) {
+        const int64_t p = c0 + tid;
+        int s = 0, len = 0;
+        double bval = 0.0;
+        if (p < p1) {
+          const int2 ce = cmap[irB[p]];
+          if (ce.y > 0) {
+            const int a = lower_bound_g(irA, ce.x, ce.x + ce.y, lo);
+            const int z = lower_bound_g(irA, a, ce.x + ce.y, hi);
+            s = a;
+            len = z - a;
           }
-          h = (h + 1) & (T - 1);
+          bval = valB[p];
         }
+        const int ex = block_excl_scan<BS>(len, tmp, &total);
+        pref[tid] = ex;
+        if (tid == BS - 1) pref[BS] = total;
+        st[tid] = s;
+        bv[tid] = bval;
+        __syncthreads();
+      } else {
+        total = pref[BS];  // staging of the single chunk is reused by pass 2
       }
+      slab_products<SR>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+      __syncthreads();
     }
-    __syncthreads();
+    if (pass == 0) {
+      // ranks: exclusive prefix of popcounts over the slab's words
+      constexpr int WPT = SLAB_WORDS / BS;
+      int c[WPT];
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < WPT; ++k) {
+        const int w = tid * WPT + k;
+        c[k] = (w < words) ? __popc(bm[w]) : 0;
+        sum += c[k];
+      }
+      int total;
+      int run = block_excl_scan<BS>(sum, tmp, &total);
+#pragma unroll
+      for (int k = 0; k < WPT; ++k) {
+        const int w = tid * WPT + k;
+        if (w < words) wpre[w] = (unsigned short)run;
+        run += c[k];
+      }
+      __syncthreads();
+    }
   }
-  if (dense) {
-    // ordered compaction of the bitmap: rows come out ascending
-    const int words = (hi - lo + 31) >> 5;
-    const unsigned wv = (tid < words) ? bm[tid] : 0u;
-    int total;
-    int pos = block_excl_scan<BS>(__popc(wv), tmp, &total);
-    unsigned x = wv;
+  // rows: each word emits its set bits at their ranks; values: coalesced copy
+  for (int w = tid; w < words; w += BS) {
+    unsigned x = bm[w];
+    int pos = wpre[w];
     while (x) {
       const int bit = __ffs(x) - 1;
       x &= x - 1;
-      const int r = tid * 32 + bit;
-      out_ir[obase + pos] = lo + r;
-      out_val[obase + pos] = acc[r];
+      out_ir[obase + pos] = lo + w * 32 + bit;
       ++pos;
     }
-  } else {
-    bitonic_sort_kv<T, BS>(keys, acc, tid, BlockSync());
-    for (int j = tid; j < nout; j += BS) {
-      out_ir[obase + j] = keys[j];
-      out_val[obase + j] = acc[j];
-    }
   }
+  for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
 }
 
 // ----------------------------------------------------------------------------
