@@ -85,6 +85,67 @@ __device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
   return lo;
 }
 
+// Flattened product loop over a staged chunk of B entries.  pref[0..nseg] is
+// the prefix sum of the segment lengths (A sub-columns); product u belongs to
+// segment sg with pref[sg] <= u < pref[sg+1].  Lanes of a wave take
+// consecutive products (coalesced reads of A's columns) and keep a per-lane
+// segment cursor that only moves forward; the segment's data (SEG, from
+// seg(sg)) is cached in registers while the cursor stays, so a product costs
+// its global loads and its apply() only.  Two products per lane are in flight
+// per iteration (load() both, then apply() both) for memory-level parallelism.
+//   seg(sg)        -> SEG           (per segment, e.g. {A offset, B value})
+//   load(SEG, u)   -> X             (global loads of product u)
+//   apply(X)                        (LDS update)
+template <class S, class L, class A>
+__device__ __forceinline__ void wave_products(const int* pref, int nseg, int u0, int u1, S&& seg, L&& load, A&& apply) {
+  int u = u0 + lane_id();
+  if (u >= u1) return;
+  int sg = seg_search(pref, nseg, u);
+  int nxt = pref[sg + 1];
+  auto cur = seg(sg);
+  for (; u + WAVE < u1; u += 2 * WAVE) {
+    if (u >= nxt) {
+      do nxt = pref[++sg + 1]; while (u >= nxt);
+      cur = seg(sg);
+    }
+    auto x0 = load(cur, u);
+    const int v = u + WAVE;
+    if (v >= nxt) {
+      do nxt = pref[++sg + 1]; while (v >= nxt);
+      cur = seg(sg);
+    }
+    auto x1 = load(cur, v);
+    apply(x0);
+    apply(x1);
+  }
+  if (u < u1) {
+    if (u >= nxt) {
+      do nxt = pref[++sg + 1]; while (u >= nxt);
+      cur = seg(sg);
+    }
+    apply(load(cur, u));
+  }
+}
+
+// block-wide version: wave w takes the contiguous range [w*per, (w+1)*per)
+template <int BS, class S, class L, class A>
+__device__ __forceinline__ void block_products(const int* pref, int total, S&& seg, L&& load, A&& apply) {
+  constexpr int NW = BS / WAVE;
+  const int w = threadIdx.x / WAVE;
+  const int per = (total + NW - 1) / NW;
+  const int u0 = min(w * per, total), u1 = min(u0 + per, total);
+  wave_products(pref, BS, u0, u1, seg, load, apply);
+}
+
+// per-segment register cache: A offset (st[sg] - pref[sg]) and B value
+struct SegI {
+  int off;
+};
+struct SegV {
+  int off;
+  double b;
+};
+
 // first position in sorted a[lo,hi) with a[pos] >= key
 __device__ __forceinline__ int lower_bound_g(const int32_t* __restrict__ a, int lo, int hi, int key) {
   while (lo < hi) {

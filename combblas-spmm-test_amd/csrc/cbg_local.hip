@@ -89,6 +89,26 @@ __global__ void k_bin_scatter(int64_t n, const uint8_t* __restrict__ bin, int nb
   if (i < n) perm[lb[b] + slot] = (int32_t)i;
 }
 
+struct RowVal {
+  int row;
+  double v;
+};
+
+// insert-or-accumulate into an LDS hash table (linear probing)
+template <int SR, int LOGT>
+__device__ __forceinline__ void hash_acc(int* keys, double* vals, int row, double v) {
+  constexpr int T = 1 << LOGT;
+  unsigned h = hash_slot<LOGT>(row);
+  while (true) {
+    const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+    if (old == EMPTY_KEY || old == row) {
+      Sem<SR>::lds_acc(&vals[h], v);
+      return;
+    }
+    h = (h + 1) & (T - 1);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // symbolic: wave per column, LDS hash of row ids
 // ----------------------------------------------------------------------------
@@ -129,17 +149,18 @@ __global__ __launch_bounds__(256) void k_sym_wave(const int32_t* __restrict__ pe
     if (lane == 0) pref[0] = 0;
     st[lane] = s;
     wave_sync();
-    for (int u = lane; u < total; u += WAVE) {
-      const int sg = seg_search(pref, WAVE, u);
-      const int row = irA[st[sg] + (u - pref[sg])];
-      unsigned h = hash_slot<LOGT>(row);
-      while (true) {
-        const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-        if (old == EMPTY_KEY) { ++count; break; }
-        if (old == row) break;
-        h = (h + 1) & (T - 1);
-      }
-    }
+    wave_products(
+        pref, WAVE, 0, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        [&](const SegI& g, int u) { return irA[g.off + u]; },
+        [&](int row) {
+          unsigned h = hash_slot<LOGT>(row);
+          while (true) {
+            const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+            if (old == EMPTY_KEY) { ++count; break; }
+            if (old == row) break;
+            h = (h + 1) & (T - 1);
+          }
+        });
     wave_sync();
   }
   count = wave_sum(count);
@@ -185,17 +206,18 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = s;
     __syncthreads();
-    for (int u = tid; u < total; u += BS) {
-      const int sg = seg_search(pref, BS, u);
-      const int row = irA[st[sg] + (u - pref[sg])];
-      unsigned h = hash_slot<LOGT>(row);
-      while (true) {
-        const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-        if (old == EMPTY_KEY) { ++count; break; }
-        if (old == row) break;
-        h = (h + 1) & (T - 1);
-      }
-    }
+    block_products<BS>(
+        pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        [&](const SegI& g, int u) { return irA[g.off + u]; },
+        [&](int row) {
+          unsigned h = hash_slot<LOGT>(row);
+          while (true) {
+            const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+            if (old == EMPTY_KEY) { ++count; break; }
+            if (old == row) break;
+            h = (h + 1) & (T - 1);
+          }
+        });
     __syncthreads();
   }
   count = wave_sum(count);
@@ -208,7 +230,7 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
 // symbolic for big columns: LDS bitmap over row passes + slab plan
 // ----------------------------------------------------------------------------
 constexpr int FINE_LOG = 13;            // fine row range = 8192 rows = 256 bitmap words
-constexpr int SLAB_CAP = 12288;         // max nnz of a slab (LDS value array, 96 KiB)
+constexpr int SLAB_CAP = 12032;         // max nnz of a slab (LDS value array, 94 KiB)
 constexpr int SLAB_SPAN_LOG = 18;       // max rows of a slab (LDS bitmap, 32 KiB)
 constexpr int SLAB_WORDS = 1 << (SLAB_SPAN_LOG - 5);
 constexpr int BIG_BS = 1024;
@@ -257,11 +279,10 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
       if (tid == BS - 1) pref[BS] = total;
       st[tid] = s;
       __syncthreads();
-      for (int u = tid; u < total; u += BS) {
-        const int sg = seg_search(pref, BS, u);
-        const int row = irA[st[sg] + (u - pref[sg])] - R0;
-        atomicOr(&bm[row >> 5], 1u << (row & 31));
-      }
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
+          [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
       __syncthreads();
     }
     // per fine range popcounts
@@ -358,21 +379,10 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
     st[lane] = s;
     bv[lane] = bval;
     wave_sync();
-    for (int u = lane; u < total; u += WAVE) {
-      const int sg = seg_search(pref, WAVE, u);
-      const int q = st[sg] + (u - pref[sg]);
-      const int row = irA[q];
-      const double v = Sem<SR>::mul(valA[q], bv[sg]);
-      unsigned h = hash_slot<LOGT>(row);
-      while (true) {
-        const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-        if (old == EMPTY_KEY || old == row) {
-          Sem<SR>::lds_acc(&vals[h], v);
-          break;
-        }
-        h = (h + 1) & (T - 1);
-      }
-    }
+    wave_products(
+        pref, WAVE, 0, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     wave_sync();
   }
   bitonic_sort_kv<T, WAVE>(keys, vals, lane, WaveSync());
@@ -430,21 +440,10 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
     st[tid] = s;
     bv[tid] = bval;
     __syncthreads();
-    for (int u = tid; u < total; u += BS) {
-      const int sg = seg_search(pref, BS, u);
-      const int q = st[sg] + (u - pref[sg]);
-      const int row = irA[q];
-      const double v = Sem<SR>::mul(valA[q], bv[sg]);
-      unsigned h = hash_slot<LOGT>(row);
-      while (true) {
-        const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-        if (old == EMPTY_KEY || old == row) {
-          Sem<SR>::lds_acc(&vals[h], v);
-          break;
-        }
-        h = (h + 1) & (T - 1);
-      }
-    }
+    block_products<BS>(
+        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     __syncthreads();
   }
   bitonic_sort_kv<T, BS>(keys, vals, tid, BlockSync());
@@ -460,7 +459,7 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 // Pass 1 marks the slab's rows in an LDS bitmap, a scan turns the bitmap into
 // ranks (= output positions, rows ascending), pass 2 accumulates each product
 // into the LDS value slot of its rank.  No hashing, no sort, coalesced output.
-constexpr int SLAB_BS = 512;
+constexpr int SLAB_BS = 1024;
 constexpr int SLAB_LDS_BYTES = SLAB_CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + SLAB_BS * 8 + (SLAB_BS + 4) * 4 +
                                SLAB_BS * 4 + (SLAB_BS / WAVE + 4) * 4;
 static_assert(SLAB_LDS_BYTES <= 160 * 1024, "slab LDS");
@@ -470,18 +469,20 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
                                               const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
   constexpr int BS = SLAB_BS;
-  for (int u = threadIdx.x; u < total; u += BS) {
-    const int sg = seg_search(pref, BS, u);
-    const int q = st[sg] + (u - pref[sg]);
-    const int r = irA[q] - lo;
-    const int w = r >> 5;
-    const unsigned bit = 1u << (r & 31);
-    if (pass == 0) {
-      atomicOr(&bm[w], bit);
-    } else {
-      const int pos = wpre[w] + __popc(bm[w] & (bit - 1u));
-      Sem<SR>::lds_acc(&vals[pos], Sem<SR>::mul(valA[q], bv[sg]));
-    }
+  if (pass == 0) {
+    block_products<BS>(
+        pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        [&](const SegI& g, int u) { return irA[g.off + u] - lo; },
+        [&](int r) { atomicOr(&bm[r >> 5], 1u << (r & 31)); });
+  } else {
+    block_products<BS>(
+        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        [&](const SegV& g, int u) { return RowVal{irA[g.off + u] - lo, Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const RowVal& x) {
+          const int w = x.row >> 5;
+          const int pos = wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u));
+          Sem<SR>::lds_acc(&vals[pos], x.v);
+        });
   }
 }
 
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ l
                                                       const double* __restrict__ valB, const int2* __restrict__ cmap,
                                                       const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                       const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
-                                                      double* __restrict__ out_val) {
+                                                      double* __restrict__ out_val, int64_t m_rows) {
   constexpr int BS = SLAB_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [SLAB_CAP]
@@ -510,6 +511,7 @@ __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ l
   const int lo = d.x, hi = d.y;
   const int words = (hi - lo + 31) >> 5;
   const int64_t obase = colptr[col] + d.z;
+  const bool full_range = (lo == 0) && ((int64_t)hi >= m_rows);
   for (int j = tid; j < words; j += BS) bm[j] = 0u;
   for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
   __syncthreads();
@@ -524,7 +526,10 @@ __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ l
         double bval = 0.0;
         if (p < p1) {
           const int2 ce = cmap[irB[p]];
-          if (ce.y > 0) {
+          if (full_range) {
+            s = ce.x;
+            len = ce.y;
+          } else if (ce.y > 0) {
             const int a = lower_bound_g(irA, ce.x, ce.x + ce.y, lo);
             const int z = lower_bound_g(irA, a, ce.x + ce.y, hi);
             s = a;
@@ -613,7 +618,18 @@ static void set_lds(K kernel, size_t bytes) {
 //  0: F == 0 | 1: <=32 wave T64 | 2: <=128 wave T256 | 3: <=512 wave T1024 |
 //  4: <=1024 block T2048 | 5: <=2048 block T4096 | 6: <=4096 block T8192 | 7: big
 static const int64_t kSymThr[] = {0, 32, 128, 512, 1024, 2048, 4096};
-static constexpr int64_t kBigFlops = 4096;
+// columns with more flops than this take the bitmap+rank slab path (runtime
+// override: CBG_BIG_FLOPS); it must stay <= 4096 so that every other column's
+// nnz fits the largest numeric hash bin
+static int64_t big_flops(int64_t m) {
+  static const char* e = getenv("CBG_BIG_FLOPS");
+  // bitmap slabs pay ~m/32 words of fixed LDS work per slab: worth it from
+  // about F >= m/256 (tuned on scale-18 R-MAT: 1024 at m = 2^18)
+  int64_t b = e ? atoll(e) : std::max<int64_t>(1024, std::min<int64_t>(4096, m / 256));
+  if (b < 64) b = 64;
+  if (b > 4096) b = 4096;
+  return b;
+}
 // bins of the numeric phase (key = exact nnz, big columns forced to the last bin)
 //  0: 0 | 1: <=32 wave T64 | 2: <=64 wave T128 | 3: <=128 wave T256 | 4: <=256 wave T512 |
 //  5: <=512 block T1024 | 6: <=1024 block T2048 | 7: <=2048 block T4096 | 8: <=4096 block T8192 | 9: big
@@ -660,14 +676,14 @@ struct Binned {
 };
 
 static void bin_columns(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr, int nthr,
-                        Binned& out, hipStream_t s) {
+                        int64_t big, Binned& out, hipStream_t s) {
   BinThr bt;
   bt.nb = nthr + 1;
-  for (int i = 0; i < nthr; ++i) bt.t[i] = thr[i];
+  for (int i = 0; i < nthr; ++i) bt.t[i] = (mode == 0) ? std::min(thr[i], big) : thr[i];
   DBuf<uint8_t> bin(n);
   DBuf<int> hist(2 * MAXBINS);
   CBG_HIP(hipMemsetAsync(hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
-  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, kBigFlops, bt, bin.p,
+  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, big, bt, bin.p,
                      hist.p);
   std::vector<int> h(MAXBINS);
   CBG_HIP(hipMemcpyAsync(h.data(), hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
@@ -751,7 +767,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
   Binned sb;
-  bin_columns(nz, flops.p, cnt.p, 0, kSymThr, 7, sb, s);
+  const int64_t big = big_flops(A.m);
+  bin_columns(nz, flops.p, cnt.p, 0, kSymThr, 7, big, sb, s);
   {
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
@@ -804,18 +821,18 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   C.val = static_cast<double*>(pool().alloc(sizeof(double) * std::max<int64_t>(nnzc, 1)));
   // numeric
   Binned nbn;
-  bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, nbn, s);
+  bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) {
       set_lds(k_num_slab<1>, SLAB_LDS_BYTES);
       hipLaunchKernelGGL(k_num_slab<1>, dim3((unsigned)nslabs), dim3(SLAB_BS), SLAB_LDS_BYTES, s, slist.p, perm_big,
-                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
+                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val, A.m);
     } else {
       set_lds(k_num_slab<0>, SLAB_LDS_BYTES);
       hipLaunchKernelGGL(k_num_slab<0>, dim3((unsigned)nslabs), dim3(SLAB_BS), SLAB_LDS_BYTES, s, slist.p, perm_big,
-                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
+                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val, A.m);
     }
   }
   // compaction of C's columns
