@@ -320,12 +320,26 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
   }
 }
 
-__global__ void k_slab_list(int nbig, const int32_t* __restrict__ nslab, const int64_t* __restrict__ base,
-                            int2* __restrict__ list) {
-  int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbig) return;
-  const int64_t o = base[b];
-  for (int s = 0; s < nslab[b]; ++s) list[o + s] = make_int2(b, s);
+// slab work lists, one per launch class (small: nnz <= small_cap)
+__global__ void k_slab_list(int nbig, const int32_t* __restrict__ nslab, const int4* __restrict__ desc, int nfine,
+                            int small_cap, int2* __restrict__ small_list, int2* __restrict__ large_list,
+                            int* __restrict__ counters) {
+  __shared__ int lc[2], lb[2];
+  if (threadIdx.x < 2) lc[threadIdx.x] = 0;
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ns = (b < nbig) ? nslab[b] : 0;
+  int nsm = 0;
+  for (int s = 0; s < ns; ++s) nsm += desc[(int64_t)b * nfine + s].w <= small_cap;
+  const int o0 = atomicAdd(&lc[0], nsm), o1 = atomicAdd(&lc[1], ns - nsm);
+  __syncthreads();
+  if (threadIdx.x < 2) lb[threadIdx.x] = atomicAdd(&counters[threadIdx.x], lc[threadIdx.x]);
+  __syncthreads();
+  int a0 = lb[0] + o0, a1 = lb[1] + o1;
+  for (int s = 0; s < ns; ++s) {
+    if (desc[(int64_t)b * nfine + s].w <= small_cap) small_list[a0++] = make_int2(b, s);
+    else large_list[a1++] = make_int2(b, s);
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -459,16 +473,21 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 // Pass 1 marks the slab's rows in an LDS bitmap, a scan turns the bitmap into
 // ranks (= output positions, rows ascending), pass 2 accumulates each product
 // into the LDS value slot of its rank.  No hashing, no sort, coalesced output.
-constexpr int SLAB_BS = 1024;
-constexpr int SLAB_LDS_BYTES = SLAB_CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + SLAB_BS * 8 + (SLAB_BS + 4) * 4 +
-                               SLAB_BS * 4 + (SLAB_BS / WAVE + 4) * 4;
-static_assert(SLAB_LDS_BYTES <= 160 * 1024, "slab LDS");
+// Two launch classes by slab size so that small slabs run 2 workgroups per CU
+// (their phases overlap) while large ones get the full LDS for values.
+template <int CAP, int BS>
+struct SlabLds {
+  static constexpr int BYTES =
+      CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4;
+  static_assert(BYTES <= 160 * 1024, "slab LDS");
+};
+constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
+constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = 1024;
 
-template <int SR>
+template <int SR, int BS>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
                                               const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
-  constexpr int BS = SLAB_BS;
   if (pass == 0) {
     block_products<BS>(
         pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
@@ -486,18 +505,17 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
   }
 }
 
-template <int SR>
-__global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
+template <int SR, int CAP, int BS>
+__global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
                                                       const int4* __restrict__ desc, int nfine,
                                                       const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmap,
                                                       const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                       const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val, int64_t m_rows) {
-  constexpr int BS = SLAB_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* vals = reinterpret_cast<double*>(smem);                          // [SLAB_CAP]
-  double* bv = vals + SLAB_CAP;                                            // [BS]
+  double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
+  double* bv = vals + CAP;                                                 // [BS]
   unsigned* bm = reinterpret_cast<unsigned*>(bv + BS);                     // [SLAB_WORDS]
   int* pref = reinterpret_cast<int*>(bm + SLAB_WORDS);                     // [BS+1]
   int* st = pref + BS + 4;                                                 // [BS]
@@ -546,12 +564,12 @@ __global__ __launch_bounds__(SLAB_BS) void k_num_slab(const int2* __restrict__ l
       } else {
         total = pref[BS];  // staging of the single chunk is reused by pass 2
       }
-      slab_products<SR>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+      slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
       __syncthreads();
     }
     if (pass == 0) {
       // ranks: exclusive prefix of popcounts over the slab's words
-      constexpr int WPT = SLAB_WORDS / BS;
+      constexpr int WPT = (SLAB_WORDS + BS - 1) / BS;
       int c[WPT];
       int sum = 0;
 #pragma unroll
@@ -668,6 +686,26 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
   set_lds(k_num_block<LOGT, BS, SR>, lds);
   hipLaunchKernelGGL((k_num_block<LOGT, BS, SR>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, B.val, cmap, A.ir,
                      A.val, colptr, C.ir, C.val);
+}
+
+template <int SR>
+static void launch_slabs(const int2* small, int nsmall, const int2* large, int nlarge, const int32_t* perm_big,
+                         const int4* desc, int nfine, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
+                         const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+  if (nsmall > 0) {
+    constexpr int L = SlabLds<SLAB_SMALL_CAP, SLAB_SMALL_BS>::BYTES;
+    auto k = k_num_slab<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>;
+    set_lds(k, L);
+    hipLaunchKernelGGL(k, dim3((unsigned)nsmall), dim3(SLAB_SMALL_BS), L, s, small, perm_big, desc, nfine, B.cp, B.ir,
+                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m);
+  }
+  if (nlarge > 0) {
+    constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
+    auto k = k_num_slab<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>;
+    set_lds(k, L);
+    hipLaunchKernelGGL(k, dim3((unsigned)nlarge), dim3(SLAB_LARGE_BS), L, s, large, perm_big, desc, nfine, B.cp, B.ir,
+                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m);
+  }
 }
 
 struct Binned {
@@ -811,9 +849,17 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));
+  DBuf<int2> slarge;
+  int ncls[2] = {0, 0};
   if (nbig > 0 && nslabs > 0) {
     slist.reset(nslabs);
-    hipLaunchKernelGGL(k_slab_list, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, nslab.p, sbase.p, slist.p);
+    slarge.reset(nslabs);
+    DBuf<int> counters(2);
+    CBG_HIP(hipMemsetAsync(counters.p, 0, 2 * sizeof(int), s));
+    hipLaunchKernelGGL(k_slab_list, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, nslab.p, desc.p, nfine,
+                       SLAB_SMALL_CAP, slist.p, slarge.p, counters.p);
+    CBG_HIP(hipMemcpyAsync(ncls, counters.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipStreamSynchronize(s));
   }
   // output arrays
   C.nnz = nnzc;
@@ -825,15 +871,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) {
-      set_lds(k_num_slab<1>, SLAB_LDS_BYTES);
-      hipLaunchKernelGGL(k_num_slab<1>, dim3((unsigned)nslabs), dim3(SLAB_BS), SLAB_LDS_BYTES, s, slist.p, perm_big,
-                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val, A.m);
-    } else {
-      set_lds(k_num_slab<0>, SLAB_LDS_BYTES);
-      hipLaunchKernelGGL(k_num_slab<0>, dim3((unsigned)nslabs), dim3(SLAB_BS), SLAB_LDS_BYTES, s, slist.p, perm_big,
-                         desc.p, nfine, B.cp, B.ir, B.val, cmap.p, A.ir, A.val, colptr.p, C.ir, C.val, A.m);
-    }
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, s);
+    else launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, s);
   }
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
