@@ -27,6 +27,11 @@
 
 namespace cbg {
 
+// Diagnostic ablation mask (CBG_DBG env, default 0; results are WRONG when set):
+//   1: k_sym_big skips its product loop       2: k_num_slab skips pass 0 products
+//   4: k_num_slab skips pass 1 products       8: k_num_slab skips the output writes
+__constant__ int c_dbg;
+
 // ----------------------------------------------------------------------------
 // small kernels
 // ----------------------------------------------------------------------------
@@ -239,7 +244,8 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
                                                     const int32_t* __restrict__ irB, const int2* __restrict__ cmap,
                                                     const int32_t* __restrict__ irA, int64_t m, int pass_log,
                                                     int nfine, int32_t* __restrict__ cnt, int4* __restrict__ desc,
-                                                    int32_t* __restrict__ nslab) {
+                                                    int32_t* __restrict__ nslab, unsigned* __restrict__ gbm,
+                                                    int64_t gwords) {
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int pass_words = 1 << (pass_log - 5);
@@ -279,18 +285,31 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ 
       if (tid == BS - 1) pref[BS] = total;
       st[tid] = s;
       __syncthreads();
-      block_products<BS>(
+      if (!(c_dbg & 1)) block_products<BS>(
           pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
           [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
       __syncthreads();
     }
-    // per fine range popcounts
+    // per fine range popcounts: thread t owns WPT consecutive words (inside one
+    // fine range of 256 words); G lanes share a fine range and reduce by shuffles.
+    // The pass bitmap is also kept for the numeric phase when gbm is given.
     const int words_used = (R1 - R0 + 31) >> 5;
-    for (int j = tid; j < words_used; j += BS) {
-      const int c = __popc(bm[j]);
-      if (c) atomicAdd(&fine[(R0 >> FINE_LOG) + (j >> (FINE_LOG - 5))], c);
+    const int WPT = max(1, pass_words / BS);
+    const int w0 = tid * WPT;
+    int c = 0;
+    unsigned* gdst = gbm ? gbm + (int64_t)b * gwords + (R0 >> 5) : nullptr;
+    for (int k = 0; k < WPT; ++k) {
+      const int j = w0 + k;
+      if (j < words_used) {
+        const unsigned x = bm[j];
+        c += __popc(x);
+        if (gdst) gdst[j] = x;
+      }
     }
+    const int G = min(WAVE, (1 << (FINE_LOG - 5)) / WPT);
+    for (int d = 1; d < G; d <<= 1) c += __shfl_xor(c, d, WAVE);
+    if ((lane_id() & (G - 1)) == 0 && w0 < words_used && c) atomicAdd(&fine[(R0 >> FINE_LOG) + (w0 >> (FINE_LOG - 5))], c);
     __syncthreads();
   }
   if (tid == 0) {
@@ -512,7 +531,8 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
                                                       const double* __restrict__ valB, const int2* __restrict__ cmap,
                                                       const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                       const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
-                                                      double* __restrict__ out_val, int64_t m_rows) {
+                                                      double* __restrict__ out_val, int64_t m_rows,
+                                                      const unsigned* __restrict__ gbm, int64_t gwords) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
   double* bv = vals + CAP;                                                 // [BS]
@@ -530,15 +550,43 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   const int words = (hi - lo + 31) >> 5;
   const int64_t obase = colptr[col] + d.z;
   const bool full_range = (lo == 0) && ((int64_t)hi >= m_rows);
-  for (int j = tid; j < words; j += BS) bm[j] = 0u;
+  const bool have_bm = gbm != nullptr;  // bitmap kept by the symbolic phase: no marking pass
+  if (have_bm) {
+    const unsigned* src = gbm + (int64_t)e.x * gwords + (lo >> 5);
+    for (int j = tid; j < words; j += BS) bm[j] = src[j];
+  } else {
+    for (int j = tid; j < words; j += BS) bm[j] = 0u;
+  }
   for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
   __syncthreads();
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
   const bool one_chunk = (p1 - p0) <= BS;
-  for (int pass = 0; pass < 2; ++pass) {
+  const int first_pass = have_bm ? 1 : 0;
+  for (int pass = first_pass; pass < 2; ++pass) {
+    if (pass == 1) {
+      // ranks: exclusive prefix of popcounts over the slab's words
+      constexpr int WPT = (SLAB_WORDS + BS - 1) / BS;
+      int c[WPT];
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < WPT; ++k) {
+        const int w = tid * WPT + k;
+        c[k] = (w < words) ? __popc(bm[w]) : 0;
+        sum += c[k];
+      }
+      int total;
+      int run = block_excl_scan<BS>(sum, tmp, &total);
+#pragma unroll
+      for (int k = 0; k < WPT; ++k) {
+        const int w = tid * WPT + k;
+        if (w < words) wpre[w] = (unsigned short)run;
+        run += c[k];
+      }
+      __syncthreads();
+    }
     for (int64_t c0 = p0; c0 < p1; c0 += BS) {
       int total;
-      if (pass == 0 || !one_chunk) {
+      if (pass == first_pass || !one_chunk) {
         const int64_t p = c0 + tid;
         int s = 0, len = 0;
         double bval = 0.0;
@@ -562,34 +610,14 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
         bv[tid] = bval;
         __syncthreads();
       } else {
-        total = pref[BS];  // staging of the single chunk is reused by pass 2
+        total = pref[BS];  // staging of the single chunk is reused by pass 1
       }
-      slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
-      __syncthreads();
-    }
-    if (pass == 0) {
-      // ranks: exclusive prefix of popcounts over the slab's words
-      constexpr int WPT = (SLAB_WORDS + BS - 1) / BS;
-      int c[WPT];
-      int sum = 0;
-#pragma unroll
-      for (int k = 0; k < WPT; ++k) {
-        const int w = tid * WPT + k;
-        c[k] = (w < words) ? __popc(bm[w]) : 0;
-        sum += c[k];
-      }
-      int total;
-      int run = block_excl_scan<BS>(sum, tmp, &total);
-#pragma unroll
-      for (int k = 0; k < WPT; ++k) {
-        const int w = tid * WPT + k;
-        if (w < words) wpre[w] = (unsigned short)run;
-        run += c[k];
-      }
+      if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
       __syncthreads();
     }
   }
   // rows: each word emits its set bits at their ranks; values: coalesced copy
+  if (c_dbg & 8) return;
   for (int w = tid; w < words; w += BS) {
     unsigned x = bm[w];
     int pos = wpre[w];
@@ -691,21 +719,26 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
 template <int SR>
 static void launch_slabs(const int2* small, int nsmall, const int2* large, int nlarge, const int32_t* perm_big,
                          const int4* desc, int nfine, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                         const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+                         const int64_t* colptr, cbg_tile& C, const unsigned* gbm, int64_t gwords, hipStream_t s) {
   if (nsmall > 0) {
     constexpr int L = SlabLds<SLAB_SMALL_CAP, SLAB_SMALL_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>;
     set_lds(k, L);
     hipLaunchKernelGGL(k, dim3((unsigned)nsmall), dim3(SLAB_SMALL_BS), L, s, small, perm_big, desc, nfine, B.cp, B.ir,
-                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m);
+                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m, gbm, gwords);
   }
   if (nlarge > 0) {
     constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>;
     set_lds(k, L);
     hipLaunchKernelGGL(k, dim3((unsigned)nlarge), dim3(SLAB_LARGE_BS), L, s, large, perm_big, desc, nfine, B.cp, B.ir,
-                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m);
+                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m, gbm, gwords);
   }
+}
+
+static double bitmap_budget_bytes() {
+  static const char* e = getenv("CBG_BITMAP_BUDGET_GB");
+  return (e ? atof(e) : 8.0) * 1e9;
 }
 
 struct Binned {
@@ -806,6 +839,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // symbolic
   Binned sb;
   const int64_t big = big_flops(A.m);
+  {
+    static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
+    CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
+  }
   bin_columns(nz, flops.p, cnt.p, 0, kSymThr, 7, big, sb, s);
   {
     const int32_t* P = sb.perm.p;
@@ -822,6 +859,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const int nfine = (int)((A.m + (1LL << FINE_LOG) - 1) >> FINE_LOG);
   DBuf<int4> desc;
   DBuf<int32_t> nslab;
+  // keep the symbolic bitmaps of big columns for the numeric phase when they fit
+  // a budget (saves the numeric marking pass); otherwise numeric rebuilds them
+  const int64_t gwords = (A.m + 31) / 32;
+  DBuf<unsigned> gbm;
+  if (nbig > 0 && (double)nbig * gwords * 4 <= bitmap_budget_bytes()) gbm.reset((size_t)nbig * gwords);
   if (nbig > 0) {
     desc.reset((size_t)nbig * nfine);
     nslab.reset(nbig);
@@ -831,7 +873,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (lds > 160 * 1024) throw HipError("k_sym_big: LDS request too large", CBG_ERR_NOTSUPPORTED);
     set_lds(k_sym_big, lds);
     hipLaunchKernelGGL(k_sym_big, dim3(nbig), dim3(BIG_BS), lds, s, perm_big, B.cp, B.ir, cmap.p, A.ir, A.m, pass_log,
-                       nfine, cnt.p, desc.p, nslab.p);
+                       nfine, cnt.p, desc.p, nslab.p, gbm.p, gwords);
   }
   // column pointers of C
   DBuf<int64_t> colptr(nz + 1);
@@ -871,8 +913,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, s);
-    else launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, s);
+    if (semiring == CBG_MIN_PLUS)
+      launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, gbm.p,
+                      gwords, s);
+    else
+      launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, gbm.p,
+                      gwords, s);
   }
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);

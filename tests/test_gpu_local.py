@@ -175,3 +175,34 @@ def test_summa_single_rank(cbg, algo, exec_mode):
         f(A, A)
     assert e.value.code == cbg.MATRIXALIAS
     g.destroy()
+
+
+@pytest.mark.parametrize("env", [{"CBG_BITMAP_BUDGET_GB": "0"}, {"CBG_BIG_FLOPS": "64"},
+                                 {"CBG_BIG_FLOPS": "64", "CBG_BITMAP_BUDGET_GB": "0"}])
+def test_big_column_path_variants(env):
+    """Same products through the other big-column code paths (subprocess: knobs are read once)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, json
+sys.path.insert(0, "tests")
+from conftest import load_cbg
+cbg = load_cbg()
+out = {}
+for scale in (12, 14):
+    A = cbg.rmat_tile(scale, 16); B = cbg.rmat_tile(scale, 16)
+    d = cbg.LocalHybridSpGEMM(A, B).digest(); d["n_big"] = cbg.last_stats()["n_big"]
+    out[scale] = d
+print(json.dumps(out))
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, **env), cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for scale in (12, 14):
+        d = res[str(scale)]
+        g = G["rmat"][f"s{scale}_ef16"]["C_local_plus"]
+        assert d["nnz"] == g["nnz"] and d["hs"] == g["hs"] and d["hv"] == g["hv"], (env, scale)
+        assert d["n_big"] > 0
