@@ -28,7 +28,7 @@
 namespace cbg {
 
 // Diagnostic ablation mask (CBG_DBG env, default 0; results are WRONG when set):
-//   1: k_sym_big skips its product loop       2: k_num_slab skips pass 0 products
+//   1: k_sym_panel skips its product loop     2: k_num_slab skips pass 0 products
 //   4: k_num_slab skips pass 1 products       8: k_num_slab skips the output writes
 __constant__ int c_dbg;
 
@@ -232,132 +232,167 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
 }
 
 // ----------------------------------------------------------------------------
-// symbolic for big columns: LDS bitmap over row passes + slab plan
+// big columns: row panels x bitmap + rank
+//
+// The rows of A are cut into panels of P = 2^plog rows (P <= 2^18, so a
+// panel's bitmap is <= 32 KiB of LDS); A(:,k) restricted to panel r is a
+// contiguous run of A's column (rows are sorted), located once by
+// k_colmap_panels.  A big column j of B is then processed as R independent
+// (j, r) sub-problems: C(panel r, j) = A(panel r, :) * B(:, j), whose sorted
+// outputs concatenate in panel order.  Each (j, r) is one workgroup in the
+// symbolic (bitmap -> counts, slab plan) and numeric (bitmap -> ranks ->
+// accumulate at rank) kernels; a (j, r) holding more than SLAB_CAP nonzeros is
+// cut into row slabs of whole fine ranges.
 // ----------------------------------------------------------------------------
 constexpr int FINE_LOG = 13;            // fine row range = 8192 rows = 256 bitmap words
 constexpr int SLAB_CAP = 12032;         // max nnz of a slab (LDS value array, 94 KiB)
-constexpr int SLAB_SPAN_LOG = 18;       // max rows of a slab (LDS bitmap, 32 KiB)
-constexpr int SLAB_WORDS = 1 << (SLAB_SPAN_LOG - 5);
-constexpr int BIG_BS = 1024;
+constexpr int PANEL_LOG_MAX = 18;       // max rows of a panel (LDS bitmap, 32 KiB)
+constexpr int SLAB_WORDS = 1 << (PANEL_LOG_MAX - 5);
+constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= max slabs) per panel
+constexpr int BIG_BS = 512;
 
-__global__ __launch_bounds__(BIG_BS) void k_sym_big(const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
-                                                    const int32_t* __restrict__ irB, const int2* __restrict__ cmap,
-                                                    const int32_t* __restrict__ irA, int64_t m, int pass_log,
-                                                    int nfine, int32_t* __restrict__ cnt, int4* __restrict__ desc,
-                                                    int32_t* __restrict__ nslab, unsigned* __restrict__ gbm,
-                                                    int64_t gwords) {
+// cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r
+__global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
+                                const int32_t* __restrict__ irA, int plog, int64_t nA1, int2* __restrict__ cmapP) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  if (i >= nzcA) return;
+  const int64_t k = jcA[i], a = cpA[i], e = cpA[i + 1];
+  for (int64_t q = a + lane_id(); q < e; q += WAVE) {
+    const int pnl = irA[q] >> plog;
+    if (q == a || (irA[q - 1] >> plog) != pnl) cmapP[pnl * nA1 + k].x = (int)q;
+    if (q == e - 1 || (irA[q + 1] >> plog) != pnl) cmapP[pnl * nA1 + k].y = (int)(q + 1);
+  }
+}
+
+// symbolic of one (big column, panel): bitmap of the panel's rows, per fine
+// range counts, slab plan; optionally keeps the bitmap for the numeric phase
+__global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict__ perm_big, int R,
+                                                      const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                      const int2* __restrict__ cmapP, int64_t nA1,
+                                                      const int32_t* __restrict__ irA, int64_t m, int plog,
+                                                      int32_t* __restrict__ cnt, int32_t* __restrict__ cnt_br,
+                                                      int4* __restrict__ desc, int32_t* __restrict__ nslab,
+                                                      unsigned* __restrict__ gbm) {
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int pass_words = 1 << (pass_log - 5);
+  const int pwords = 1 << (plog - 5);
+  const int nfine = 1 << (plog - FINE_LOG);
   unsigned* bm = reinterpret_cast<unsigned*>(smem);
-  int* fine = reinterpret_cast<int*>(bm + pass_words);
-  int* pref = fine + ((nfine + 3) & ~3);
+  int* fine = reinterpret_cast<int*>(bm + pwords);
+  int* pref = fine + NFINE_MAX;
   int* st = pref + BS + 4;
   int* tmp = st + BS;
   const int tid = threadIdx.x;
-  const int b = blockIdx.x;
+  const int br = blockIdx.x;
+  const int b = br / R, r = br % R;
   const int col = perm_big[b];
-  for (int j = tid; j < nfine; j += BS) fine[j] = 0;
+  const int R0 = r << plog;
+  const int R1 = (int)min((int64_t)R0 + (1LL << plog), m);
+  const int words = (R1 - R0 + 31) >> 5;
+  const int2* cm = cmapP + (int64_t)r * nA1;
+  for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
+  if (tid < NFINE_MAX) fine[tid] = 0;
+  __syncthreads();
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
-  const int npass = (int)((m + (1LL << pass_log) - 1) >> pass_log);
-  for (int pass = 0; pass < npass; ++pass) {
-    const int R0 = pass << pass_log;
-    const int R1 = (int)min((int64_t)R0 + (1LL << pass_log), m);
-    for (int j = tid; j < pass_words; j += BS) bm[j] = 0u;
+  for (int64_t c0 = p0; c0 < p1; c0 += BS) {
+    const int64_t p = c0 + tid;
+    int s = 0, len = 0;
+    if (p < p1) {
+      const int2 e = cm[irB[p]];
+      s = e.x;
+      len = e.y - e.x;
+    }
+    int total;
+    const int ex = block_excl_scan<BS>(len, tmp, &total);
+    pref[tid] = ex;
+    if (tid == BS - 1) pref[BS] = total;
+    st[tid] = s;
     __syncthreads();
-    for (int64_t c0 = p0; c0 < p1; c0 += BS) {
-      const int64_t p = c0 + tid;
-      int s = 0, len = 0;
-      if (p < p1) {
-        int2 e = cmap[irB[p]];
-        s = e.x;
-        len = e.y;
-        if (npass > 1 && len > 0) {
-          const int a = lower_bound_g(irA, s, s + len, R0);
-          const int z = lower_bound_g(irA, a, s + len, R1);
-          s = a;
-          len = z - a;
-        }
-      }
-      int total;
-      const int ex = block_excl_scan<BS>(len, tmp, &total);
-      pref[tid] = ex;
-      if (tid == BS - 1) pref[BS] = total;
-      st[tid] = s;
-      __syncthreads();
-      if (!(c_dbg & 1)) block_products<BS>(
+    if (!(c_dbg & 1))
+      block_products<BS>(
           pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
           [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
-      __syncthreads();
-    }
-    // per fine range popcounts: thread t owns WPT consecutive words (inside one
-    // fine range of 256 words); G lanes share a fine range and reduce by shuffles.
-    // The pass bitmap is also kept for the numeric phase when gbm is given.
-    const int words_used = (R1 - R0 + 31) >> 5;
-    const int WPT = max(1, pass_words / BS);
-    const int w0 = tid * WPT;
-    int c = 0;
-    unsigned* gdst = gbm ? gbm + (int64_t)b * gwords + (R0 >> 5) : nullptr;
-    for (int k = 0; k < WPT; ++k) {
-      const int j = w0 + k;
-      if (j < words_used) {
-        const unsigned x = bm[j];
-        c += __popc(x);
-        if (gdst) gdst[j] = x;
-      }
-    }
-    const int G = min(WAVE, (1 << (FINE_LOG - 5)) / WPT);
-    for (int d = 1; d < G; d <<= 1) c += __shfl_xor(c, d, WAVE);
-    if ((lane_id() & (G - 1)) == 0 && w0 < words_used && c) atomicAdd(&fine[(R0 >> FINE_LOG) + (w0 >> (FINE_LOG - 5))], c);
     __syncthreads();
   }
+  // per fine range popcounts: thread t owns WPT consecutive words inside one
+  // fine range (256 words); G lanes share a fine range and reduce by shuffles
+  const int WPT = max(1, pwords / BS);
+  const int w0 = tid * WPT;
+  int c = 0;
+  unsigned* gdst = gbm ? gbm + (int64_t)br * SLAB_WORDS : nullptr;
+  for (int k = 0; k < WPT; ++k) {
+    const int j = w0 + k;
+    if (j < words) {
+      const unsigned x = bm[j];
+      c += __popc(x);
+      if (gdst) gdst[j] = x;
+    }
+  }
+  const int G = min(WAVE, (1 << (FINE_LOG - 5)) / WPT);
+  for (int d = 1; d < G; d <<= 1) c += __shfl_xor(c, d, WAVE);
+  if ((lane_id() & (G - 1)) == 0 && w0 < words && c) atomicAdd(&fine[w0 >> (FINE_LOG - 5)], c);
+  __syncthreads();
   if (tid == 0) {
-    // greedy slab plan over fine ranges: consecutive ranges while the slab
-    // holds <= SLAB_CAP nonzeros and spans <= 2^SLAB_SPAN_LOG rows
-    int total = 0, ns = 0, off = 0;
+    // greedy slab plan: consecutive fine ranges while the slab holds <= SLAB_CAP
+    int total = 0, ns = 0;
     int g_lo = -1, g_hi = 0, g_cnt = 0;
-    int4* d = desc + (int64_t)b * nfine;
+    int4* d = desc + (int64_t)br * NFINE_MAX;
     for (int f = 0; f < nfine; ++f) {
-      const int c = fine[f];
-      total += c;
-      if (c == 0) continue;
-      const int lo = f << FINE_LOG;
-      const int hi = (int)min((int64_t)(f + 1) << FINE_LOG, m);
-      if (g_cnt && (g_cnt + c > SLAB_CAP || hi - g_lo > (1 << SLAB_SPAN_LOG))) {
-        d[ns++] = make_int4(g_lo, g_hi, off, g_cnt);
-        off += g_cnt;
+      const int cf = fine[f];
+      if (cf == 0) continue;
+      const int lo = R0 + (f << FINE_LOG);
+      const int hi = min(lo + (1 << FINE_LOG), R1);
+      if (g_cnt && g_cnt + cf > SLAB_CAP) {
+        d[ns++] = make_int4(g_lo, g_hi, total - g_cnt, g_cnt);
         g_cnt = 0;
       }
       if (g_cnt == 0) g_lo = lo;
       g_hi = hi;
-      g_cnt += c;
+      g_cnt += cf;
+      total += cf;
     }
-    if (g_cnt) d[ns++] = make_int4(g_lo, g_hi, off, g_cnt);
-    cnt[col] = total;
-    nslab[b] = ns;
+    if (g_cnt) d[ns++] = make_int4(g_lo, g_hi, total - g_cnt, g_cnt);
+    cnt_br[br] = total;
+    nslab[br] = ns;
+    if (total) atomicAdd(&cnt[col], total);
   }
 }
 
-// slab work lists, one per launch class (small: nnz <= small_cap)
-__global__ void k_slab_list(int nbig, const int32_t* __restrict__ nslab, const int4* __restrict__ desc, int nfine,
-                            int small_cap, int2* __restrict__ small_list, int2* __restrict__ large_list,
-                            int* __restrict__ counters) {
+// slab work lists per launch class (small: nnz <= small_cap); turns the
+// within-panel offsets of the slab plan into within-column offsets
+__global__ void k_slab_list(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
+                            int4* __restrict__ desc, int small_cap, int2* __restrict__ small_list,
+                            int2* __restrict__ large_list, int* __restrict__ counters) {
   __shared__ int lc[2], lb[2];
   if (threadIdx.x < 2) lc[threadIdx.x] = 0;
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ns = (b < nbig) ? nslab[b] : 0;
-  int nsm = 0;
-  for (int s = 0; s < ns; ++s) nsm += desc[(int64_t)b * nfine + s].w <= small_cap;
-  const int o0 = atomicAdd(&lc[0], nsm), o1 = atomicAdd(&lc[1], ns - nsm);
+  int nsm = 0, nl = 0;
+  if (b < nbig) {
+    int off = 0;
+    for (int r = 0; r < R; ++r) {
+      const int br = b * R + r;
+      for (int s = 0; s < nslab[br]; ++s) {
+        int4& d = desc[(int64_t)br * NFINE_MAX + s];
+        d.z += off;
+        if (d.w <= small_cap) ++nsm; else ++nl;
+      }
+      off += cnt_br[br];
+    }
+  }
+  const int o0 = atomicAdd(&lc[0], nsm), o1 = atomicAdd(&lc[1], nl);
   __syncthreads();
   if (threadIdx.x < 2) lb[threadIdx.x] = atomicAdd(&counters[threadIdx.x], lc[threadIdx.x]);
   __syncthreads();
+  if (b >= nbig) return;
   int a0 = lb[0] + o0, a1 = lb[1] + o1;
-  for (int s = 0; s < ns; ++s) {
-    if (desc[(int64_t)b * nfine + s].w <= small_cap) small_list[a0++] = make_int2(b, s);
-    else large_list[a1++] = make_int2(b, s);
+  for (int r = 0; r < R; ++r) {
+    const int br = b * R + r;
+    for (int s = 0; s < nslab[br]; ++s) {
+      if (desc[(int64_t)br * NFINE_MAX + s].w <= small_cap) small_list[a0++] = make_int2(br, s);
+      else large_list[a1++] = make_int2(br, s);
+    }
   }
 }
 
@@ -526,13 +561,13 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
 
 template <int SR, int CAP, int BS>
 __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
-                                                      const int4* __restrict__ desc, int nfine,
-                                                      const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                      const double* __restrict__ valB, const int2* __restrict__ cmap,
-                                                      const int32_t* __restrict__ irA, const double* __restrict__ valA,
-                                                      const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
-                                                      double* __restrict__ out_val, int64_t m_rows,
-                                                      const unsigned* __restrict__ gbm, int64_t gwords) {
+                                                 const int4* __restrict__ desc, int R, int plog,
+                                                 const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                 const double* __restrict__ valB, const int2* __restrict__ cmapP,
+                                                 int64_t nA1, const int32_t* __restrict__ irA,
+                                                 const double* __restrict__ valA, const int64_t* __restrict__ colptr,
+                                                 int32_t* __restrict__ out_ir, double* __restrict__ out_val,
+                                                 int64_t m_rows, const unsigned* __restrict__ gbm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
   double* bv = vals + CAP;                                                 // [BS]
@@ -542,17 +577,21 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   int* tmp = st + BS;                                                      // scan scratch
   unsigned short* wpre = reinterpret_cast<unsigned short*>(tmp + BS / WAVE + 4);  // [SLAB_WORDS]
   const int tid = threadIdx.x;
-  const int2 e = list[blockIdx.x];
-  const int4 d = desc[(int64_t)e.x * nfine + e.y];
-  const int col = perm_big[e.x];
+  const int2 e = list[blockIdx.x];  // (big column * R + panel, slab)
+  const int4 d = desc[(int64_t)e.x * NFINE_MAX + e.y];
+  const int col = perm_big[e.x / R];
+  const int r = e.x % R;
+  const int R0 = r << plog;
+  const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
+  const int2* cm = cmapP + (int64_t)r * nA1;
   const int nout = d.w;
   const int lo = d.x, hi = d.y;
   const int words = (hi - lo + 31) >> 5;
   const int64_t obase = colptr[col] + d.z;
-  const bool full_range = (lo == 0) && ((int64_t)hi >= m_rows);
+  const bool full_range = (lo == R0) && (hi == R1);  // the slab is the whole panel
   const bool have_bm = gbm != nullptr;  // bitmap kept by the symbolic phase: no marking pass
   if (have_bm) {
-    const unsigned* src = gbm + (int64_t)e.x * gwords + (lo >> 5);
+    const unsigned* src = gbm + (int64_t)e.x * SLAB_WORDS + ((lo - R0) >> 5);
     for (int j = tid; j < words; j += BS) bm[j] = src[j];
   } else {
     for (int j = tid; j < words; j += BS) bm[j] = 0u;
@@ -591,13 +630,13 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
         int s = 0, len = 0;
         double bval = 0.0;
         if (p < p1) {
-          const int2 ce = cmap[irB[p]];
+          const int2 ce = cm[irB[p]];
           if (full_range) {
             s = ce.x;
-            len = ce.y;
-          } else if (ce.y > 0) {
-            const int a = lower_bound_g(irA, ce.x, ce.x + ce.y, lo);
-            const int z = lower_bound_g(irA, a, ce.x + ce.y, hi);
+            len = ce.y - ce.x;
+          } else if (ce.y > ce.x) {
+            const int a = lower_bound_g(irA, ce.x, ce.y, lo);
+            const int z = lower_bound_g(irA, a, ce.y, hi);
             s = a;
             len = z - a;
           }
@@ -716,23 +755,33 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
                      A.val, colptr, C.ir, C.val);
 }
 
+struct BigPlan {
+  int nbig = 0, R = 1, plog = 0;
+  const int32_t* perm_big = nullptr;
+  DBuf<int2> cmapP;
+  DBuf<int4> desc;
+  DBuf<int32_t> nslab, cnt_br;
+  DBuf<unsigned> gbm;
+};
+
 template <int SR>
-static void launch_slabs(const int2* small, int nsmall, const int2* large, int nlarge, const int32_t* perm_big,
-                         const int4* desc, int nfine, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                         const int64_t* colptr, cbg_tile& C, const unsigned* gbm, int64_t gwords, hipStream_t s) {
+static void launch_slabs(const int2* small, int nsmall, const int2* large, int nlarge, const BigPlan& bp,
+                         const cbg_tile& A, const cbg_tile& B, const int64_t* colptr, cbg_tile& C, hipStream_t s) {
   if (nsmall > 0) {
     constexpr int L = SlabLds<SLAB_SMALL_CAP, SLAB_SMALL_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>;
     set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)nsmall), dim3(SLAB_SMALL_BS), L, s, small, perm_big, desc, nfine, B.cp, B.ir,
-                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m, gbm, gwords);
+    hipLaunchKernelGGL(k, dim3((unsigned)nsmall), dim3(SLAB_SMALL_BS), L, s, small, bp.perm_big, bp.desc.p, bp.R,
+                       bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
+                       bp.gbm.p);
   }
   if (nlarge > 0) {
     constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>;
     set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)nlarge), dim3(SLAB_LARGE_BS), L, s, large, perm_big, desc, nfine, B.cp, B.ir,
-                       B.val, cmap, A.ir, A.val, colptr, C.ir, C.val, A.m, gbm, gwords);
+    hipLaunchKernelGGL(k, dim3((unsigned)nlarge), dim3(SLAB_LARGE_BS), L, s, large, bp.perm_big, bp.desc.p, bp.R,
+                       bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
+                       bp.gbm.p);
   }
 }
 
@@ -772,9 +821,9 @@ static void bin_columns(int64_t n, const int64_t* flops, const int32_t* cnt, int
   CBG_HIP(hipStreamSynchronize(s));  // `bin`/`hist` are released on return
 }
 
-static int pick_pass_log(int64_t m) {
+static int pick_panel_log(int64_t m) {
   int l = FINE_LOG;
-  while ((1LL << l) < m && l < 20) ++l;
+  while ((1LL << l) < m && l < PANEL_LOG_MAX) ++l;
   return l;
 }
 
@@ -854,52 +903,56 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, s);
     launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, s);
   }
-  const int nbig = sb.count[7];
-  const int32_t* perm_big = sb.perm.p + sb.offset[7];
-  const int nfine = (int)((A.m + (1LL << FINE_LOG) - 1) >> FINE_LOG);
-  DBuf<int4> desc;
-  DBuf<int32_t> nslab;
-  // keep the symbolic bitmaps of big columns for the numeric phase when they fit
-  // a budget (saves the numeric marking pass); otherwise numeric rebuilds them
-  const int64_t gwords = (A.m + 31) / 32;
-  DBuf<unsigned> gbm;
-  if (nbig > 0 && (double)nbig * gwords * 4 <= bitmap_budget_bytes()) gbm.reset((size_t)nbig * gwords);
+  BigPlan bp;
+  bp.nbig = sb.count[7];
+  bp.perm_big = sb.perm.p + sb.offset[7];
+  bp.plog = pick_panel_log(A.m);
+  bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
+  const int nbig = bp.nbig;
+  const int64_t nbr = (int64_t)nbig * bp.R;
   if (nbig > 0) {
-    desc.reset((size_t)nbig * nfine);
-    nslab.reset(nbig);
-    const int pass_log = pick_pass_log(A.m);
-    const size_t lds = (size_t)(1 << (pass_log - 5)) * 4 + (size_t)((nfine + 3) & ~3) * 4 + (BIG_BS + 4) * 4 +
-                       BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4;
-    if (lds > 160 * 1024) throw HipError("k_sym_big: LDS request too large", CBG_ERR_NOTSUPPORTED);
-    set_lds(k_sym_big, lds);
-    hipLaunchKernelGGL(k_sym_big, dim3(nbig), dim3(BIG_BS), lds, s, perm_big, B.cp, B.ir, cmap.p, A.ir, A.m, pass_log,
-                       nfine, cnt.p, desc.p, nslab.p, gbm.p, gwords);
+    // panel column maps of A
+    bp.cmapP.reset((size_t)bp.R * (A.n + 1));
+    CBG_HIP(hipMemsetAsync(bp.cmapP.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
+    hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * WAVE, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
+                       bp.plog, A.n + 1, bp.cmapP.p);
+    bp.desc.reset((size_t)nbr * NFINE_MAX);
+    bp.nslab.reset(nbr);
+    bp.cnt_br.reset(nbr);
+    // keep the symbolic bitmaps for the numeric phase when they fit a budget
+    // (saves the numeric marking pass); otherwise numeric rebuilds them
+    if ((double)nbr * SLAB_WORDS * 4 <= bitmap_budget_bytes()) bp.gbm.reset((size_t)nbr * SLAB_WORDS);
+    const size_t lds = (size_t)(1 << (bp.plog - 5)) * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 +
+                       (BIG_BS / WAVE + 4) * 4;
+    set_lds(k_sym_panel, lds);
+    if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
+    hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)nbr), dim3(BIG_BS), lds, s, bp.perm_big, bp.R, B.cp, B.ir,
+                       bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p);
   }
   // column pointers of C
   DBuf<int64_t> colptr(nz + 1);
   exclusive_scan_i32_to_i64(cnt.p, colptr.p, nz, s);
   int64_t nnzc = 0;
   CBG_HIP(hipMemcpyAsync(&nnzc, colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  // slab list of big columns
+  // slab lists of big columns
   DBuf<int64_t> sbase;
-  DBuf<int2> slist;
+  DBuf<int2> slist, slarge;
   int64_t nslabs = 0;
   if (nbig > 0) {
-    sbase.reset(nbig + 1);
-    exclusive_scan_i32_to_i64(nslab.p, sbase.p, nbig, s);
-    CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbig, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    sbase.reset(nbr + 1);
+    exclusive_scan_i32_to_i64(bp.nslab.p, sbase.p, nbr, s);
+    CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));
-  DBuf<int2> slarge;
   int ncls[2] = {0, 0};
   if (nbig > 0 && nslabs > 0) {
     slist.reset(nslabs);
     slarge.reset(nslabs);
     DBuf<int> counters(2);
     CBG_HIP(hipMemsetAsync(counters.p, 0, 2 * sizeof(int), s));
-    hipLaunchKernelGGL(k_slab_list, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, nslab.p, desc.p, nfine,
-                       SLAB_SMALL_CAP, slist.p, slarge.p, counters.p);
+    hipLaunchKernelGGL(k_slab_list, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.cnt_br.p,
+                       bp.desc.p, SLAB_SMALL_CAP, slist.p, slarge.p, counters.p);
     CBG_HIP(hipMemcpyAsync(ncls, counters.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));
   }
@@ -913,12 +966,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS)
-      launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, gbm.p,
-                      gwords, s);
-    else
-      launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], perm_big, desc.p, nfine, A, B, cmap.p, colptr.p, C, gbm.p,
-                      gwords, s);
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], bp, A, B, colptr.p, C, s);
+    else launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], bp, A, B, colptr.p, C, s);
   }
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
