@@ -708,9 +708,9 @@ static const int64_t kSymThr[] = {0, 32, 128, 512, 1024, 2048, 4096};
 // nnz fits the largest numeric hash bin
 static int64_t big_flops(int64_t m) {
   static const char* e = getenv("CBG_BIG_FLOPS");
-  // bitmap slabs pay ~m/32 words of fixed LDS work per slab: worth it from
-  // about F >= m/256 (tuned on scale-18 R-MAT: 1024 at m = 2^18)
-  int64_t b = e ? atoll(e) : std::max<int64_t>(1024, std::min<int64_t>(4096, m / 256));
+  // a (column, panel) bitmap costs ~P/32 words of fixed LDS work; measured on
+  // R-MAT: 1024 best at m = 2^18 (one panel), 2048 at m = 2^20 (four panels)
+  int64_t b = e ? atoll(e) : (m <= (1LL << 18) ? 1024 : 2048);
   if (b < 64) b = 64;
   if (b > 4096) b = 4096;
   return b;

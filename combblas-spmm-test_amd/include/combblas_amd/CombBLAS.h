@@ -1,0 +1,287 @@
+// combblas_amd/CombBLAS.h -- C++ mirror of the reference's SpGEMM operator
+// surface over libcbg's C ABI (include/cbg.h).  Header-only.
+//
+//   reference (include/CombBLAS/...)              this header (namespace combblas_amd)
+//   SpDCCols<IT,NT>            SpDCCols.h         SpDCCols<IT,NT>   (device DCSC tile)
+//   CommGrid(MPI_Comm,r,c)     CommGrid.h         CommGrid(MPI_Comm,r,c) -> RCCL grid
+//   SpParMat<IT,NT,DER>        SpParMat.h         SpParMat<IT,NT,DER>
+//   PlusTimesSRing/MinPlusSRing Semirings.h:212   PlusTimesSRing/MinPlusSRing
+//   LocalHybridSpGEMM          mtSpGEMM.h:212     LocalHybridSpGEMM  (returns a device SpDCCols*)
+//   Mult_AnXBn_DoubleBuff      ParFriends.h:798   Mult_AnXBn_DoubleBuff
+//   Mult_AnXBn_Synch           ParFriends.h:1004  Mult_AnXBn_Synch
+//   PSpGEMM                    SpParMat.h:454     PSpGEMM
+//
+// Same template parameters and call shapes, so MultTiming/MultTest-style
+// drivers (tools/multtiming.cpp) compile against it.  Misuse that the
+// reference MPI_Aborts on (DIMMISMATCH 3002, MATRIXALIAS 3005, NOTSQUARE 3003)
+// aborts here with the same code.  Define CBG_NO_MPI to use a single-process grid.
+#pragma once
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../../include/cbg.h"
+
+#ifndef CBG_NO_MPI
+#include <mpi.h>
+#endif
+
+namespace combblas_amd {
+
+inline void cbg_abort_on(int rc, const char* what) {
+  if (rc == CBG_OK) return;
+  std::fprintf(stderr, "%s: libcbg error %d: %s\n", what, rc, cbg_last_error());
+#ifndef CBG_NO_MPI
+  int init = 0;
+  MPI_Initialized(&init);
+  if (init) MPI_Abort(MPI_COMM_WORLD, rc);
+#endif
+  std::exit(rc);
+}
+
+// ---------------------------------------------------------------- semirings
+template <class T1, class T2>
+struct PlusTimesSRing {
+  typedef T1 T_promote;
+  static constexpr int code = CBG_PLUS_TIMES;
+  static T1 id() { return 0; }
+  static bool returnedSAID() { return false; }
+  static T1 add(const T1& a, const T1& b) { return a + b; }
+  static T1 multiply(const T1& a, const T2& b) { return a * b; }
+};
+template <class T1, class T2>
+struct MinPlusSRing {
+  typedef T1 T_promote;
+  static constexpr int code = CBG_MIN_PLUS;
+  static T1 id() { return std::numeric_limits<T1>::max(); }
+  static bool returnedSAID() { return false; }
+  static T1 add(const T1& a, const T1& b) { return b < a ? b : a; }
+  static T1 multiply(const T1& a, const T2& b) {
+    const T1 inf = std::numeric_limits<T1>::max();
+    return (a == inf || b == inf) ? inf : a + b;
+  }
+};
+
+// ---------------------------------------------------------------- tiles
+// SpDCCols<IT,NT>: a DCSC tile resident in HBM (int32 local indices, f64 values).
+template <class IT, class NT>
+class SpDCCols {
+ public:
+  typedef IT LocalIT;
+  typedef NT LocalNT;
+  static const IT esscount = 4;  // SpDCCols.cpp:45-46
+
+  SpDCCols() { t_ = cbg_tile{}; }
+  explicit SpDCCols(const cbg_tile& dev) : t_(dev) {}
+  // from column-sorted host tuples (row, col, value), as SpDCCols(nRow,nCol,nTuples,tuples,false)
+  SpDCCols(IT nRow, IT nCol, IT nTuples, const std::tuple<IT, IT, NT>* tuples, bool transpose = false) {
+    if (transpose) throw std::invalid_argument("row-sorted input is not supported");
+    std::vector<int64_t> cp(1, 0);
+    std::vector<int32_t> jc, ir(nTuples);
+    std::vector<double> val(nTuples);
+    for (IT i = 0; i < nTuples; ++i) {
+      const IT c = std::get<1>(tuples[i]);
+      if (jc.empty() || jc.back() != (int32_t)c) {
+        if (!jc.empty()) cp.push_back(i);
+        jc.push_back((int32_t)c);
+      }
+      ir[i] = (int32_t)std::get<0>(tuples[i]);
+      val[i] = (double)std::get<2>(tuples[i]);
+    }
+    cp.push_back(nTuples);
+    if (jc.empty()) cp.assign(1, 0);
+    cbg_tile h{nRow, nCol, (int64_t)nTuples, (int64_t)jc.size(), cp.data(), jc.data(), ir.data(), val.data(), 0, 0};
+    cbg_abort_on(cbg_tile_upload(&h, &t_), "SpDCCols upload");
+  }
+  ~SpDCCols() { cbg_tile_free(&t_); }
+  SpDCCols(const SpDCCols&) = delete;
+  SpDCCols& operator=(const SpDCCols&) = delete;
+
+  IT getnrow() const { return (IT)t_.m; }
+  IT getncol() const { return (IT)t_.n; }
+  int64_t getnnz() const { return t_.nnz; }
+  int64_t getnzc() const { return t_.nzc; }
+  bool isZero() const { return t_.nnz == 0; }
+  std::vector<IT> GetEssentials() const { return {(IT)t_.nnz, (IT)t_.m, (IT)t_.n, (IT)t_.nzc}; }
+  const cbg_tile* tile() const { return &t_; }
+  cbg_tile* tile() { return &t_; }
+
+  // SpDCCols::Split (SpDCCols.cpp:905-930): columns [0,n/2) and [n/2,n)
+  void Split(SpDCCols& a, SpDCCols& b) {
+    cbg_tile l{}, r{};
+    cbg_abort_on(cbg_tile_split_cols(&t_, t_.n / 2, &l, &r), "Split");
+    a.reset(l);
+    b.reset(r);
+  }
+  void reset(const cbg_tile& t) {
+    cbg_tile_free(&t_);
+    t_ = t;
+  }
+  // host copy as (cp, jc, ir, val)
+  void download(std::vector<int64_t>& cp, std::vector<int32_t>& jc, std::vector<int32_t>& ir,
+                std::vector<double>& val) const {
+    cp.resize(t_.nzc + 1);
+    jc.resize(t_.nzc);
+    ir.resize(t_.nnz);
+    val.resize(t_.nnz);
+    cbg_tile h{0, 0, 0, 0, cp.data(), jc.data(), ir.data(), val.data(), 0, 0};
+    cbg_abort_on(cbg_tile_download(&t_, &h), "download");
+  }
+
+ private:
+  cbg_tile t_;
+};
+
+// ---------------------------------------------------------------- grid
+class CommGrid {
+ public:
+#ifndef CBG_NO_MPI
+  // CommGrid(MPI_COMM_WORLD, 0, 0): square grid or NOTSQUARE (src/CommGrid.cpp:37-75).
+  // One rank per GPU; the RCCL unique id travels by MPI_Bcast.
+  CommGrid(MPI_Comm world, int nrowproc, int ncolproc) {
+    MPI_Comm_rank(world, &rank_);
+    MPI_Comm_size(world, &size_);
+    char id[CBG_UNIQUE_ID_BYTES] = {0};
+    if (rank_ == 0) cbg_abort_on(cbg_get_unique_id(id), "ncclGetUniqueId");
+    MPI_Bcast(id, CBG_UNIQUE_ID_BYTES, MPI_BYTE, 0, world);
+    int ndev = 1;
+    cbg_device_count(&ndev);
+    cbg_set_device(rank_ % (ndev > 0 ? ndev : 1));
+    cbg_abort_on(cbg_grid_create(rank_, size_, nrowproc, ncolproc, id, &g_), "CommGrid");
+    int dummy;
+    cbg_grid_info(g_, &dummy, &dummy, &rows_, &cols_, &prow_, &pcol_);
+  }
+#endif
+  // single-process 1x1 grid
+  CommGrid() {
+    static cbg_host_comm self = {[](void*, int, void*, size_t, int) { return 0; },
+                                 [](void*, int, const void* in, void* out, size_t b) {
+                                   std::memcpy(out, in, b);
+                                   return 0;
+                                 },
+                                 nullptr};
+    cbg_abort_on(cbg_grid_create_host(0, 1, 1, 1, &self, &g_), "CommGrid");
+  }
+  ~CommGrid() { cbg_grid_destroy(g_); }
+  CommGrid(const CommGrid&) = delete;
+  CommGrid& operator=(const CommGrid&) = delete;
+
+  int GetRank() const { return rank_; }
+  int GetSize() const { return size_; }
+  int GetGridRows() const { return rows_; }
+  int GetGridCols() const { return cols_; }
+  int GetRankInProcRow() const { return pcol_; }
+  int GetRankInProcCol() const { return prow_; }
+  cbg_grid* handle() const { return g_; }
+  bool operator==(const CommGrid& o) const { return rows_ == o.rows_ && cols_ == o.cols_ && size_ == o.size_; }
+
+ private:
+  cbg_grid* g_ = nullptr;
+  int rank_ = 0, size_ = 1, rows_ = 1, cols_ = 1, prow_ = 0, pcol_ = 0;
+};
+
+// ---------------------------------------------------------------- distributed matrix
+template <class IT, class NT, class DER>
+class SpParMat {
+ public:
+  SpParMat() = default;
+  SpParMat(DER* seq, std::shared_ptr<CommGrid> grid, IT gm, IT gn) : spSeq(seq), commGrid(grid), m_(gm), n_(gn) {}
+  SpParMat(SpParMat&& o) noexcept : spSeq(o.spSeq), commGrid(o.commGrid), m_(o.m_), n_(o.n_) { o.spSeq = nullptr; }
+  SpParMat& operator=(SpParMat&& o) noexcept {
+    if (this != &o) {
+      delete spSeq;
+      spSeq = o.spSeq;
+      o.spSeq = nullptr;
+      commGrid = o.commGrid;
+      m_ = o.m_;
+      n_ = o.n_;
+    }
+    return *this;
+  }
+  ~SpParMat() { delete spSeq; }
+  SpParMat(const SpParMat&) = delete;
+
+  // Graph500 R-MAT tile of this rank (GenWriteMatrix.cpp:101-114 semantics)
+  static SpParMat rmat(std::shared_ptr<CommGrid> g, int scale, int ef, uint64_t seed = 0xDECAFBADULL) {
+    cbg_tile t{};
+    cbg_abort_on(cbg_rmat_tile(scale, ef, seed, g->GetGridRows(), g->GetGridCols(), g->GetRankInProcCol(),
+                               g->GetRankInProcRow(), &t),
+                 "rmat");
+    const IT nv = (IT)1 << scale;
+    return SpParMat(new DER(t), g, nv, nv);
+  }
+
+  IT getnrow() const { return m_; }
+  IT getncol() const { return n_; }
+  int64_t getnnz() const {  // SpParMat::getnnz (Allreduce, SpParMat.cpp:772-778)
+    int64_t v = spSeq ? spSeq->getnnz() : 0;
+    cbg_abort_on(cbg_grid_allreduce_sum_i64(commGrid->handle(), &v), "getnnz");
+    return v;
+  }
+  DER& seq() const { return *spSeq; }
+  std::shared_ptr<CommGrid> getcommgrid() const { return commGrid; }
+
+  DER* spSeq = nullptr;
+  std::shared_ptr<CommGrid> commGrid;
+
+ private:
+  IT m_ = 0, n_ = 0;
+};
+
+// ---------------------------------------------------------------- products
+template <class SR, class NTO, class IT, class NT1, class NT2>
+SpDCCols<IT, NTO>* LocalHybridSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA,
+                                     bool clearB) {
+  cbg_tile c{};
+  cbg_abort_on(cbg_local_spgemm(A.tile(), B.tile(), SR::code, &c, nullptr), "LocalHybridSpGEMM");
+  if (clearA) delete const_cast<SpDCCols<IT, NT1>*>(&A);
+  if (clearB) delete const_cast<SpDCCols<IT, NT2>*>(&B);
+  return new SpDCCols<IT, NTO>(c);
+}
+
+namespace detail {
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDERA, class UDERB>
+SpParMat<IU, NUO, UDERO> summa(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B, int algo, bool clearA,
+                               bool clearB, int exec) {
+  if ((void*)&A == (void*)&B) cbg_abort_on(CBG_ERR_MATRIXALIAS, "Can not multiply, inputs alias");
+  if (A.getncol() != B.getnrow()) cbg_abort_on(CBG_ERR_DIMMISMATCH, "Can not multiply, dimensions does not match");
+  if (!(*A.commGrid == *B.commGrid)) cbg_abort_on(CBG_ERR_GRIDMISMATCH, "Grids don't confirm for multiplication");
+  cbg_tile c{};
+  cbg_abort_on(cbg_summa_spgemm(A.commGrid->handle(), A.spSeq->tile(), B.spSeq->tile(), A.getncol(), B.getnrow(),
+                                SR::code, algo, exec, &c),
+               algo == CBG_DOUBLEBUFF ? "Mult_AnXBn_DoubleBuff" : "Mult_AnXBn_Synch");
+  SpParMat<IU, NUO, UDERO> C(new UDERO(c), A.commGrid, A.getnrow(), B.getncol());
+  if (clearA) { delete A.spSeq; A.spSeq = nullptr; }
+  if (clearB) { delete B.spSeq; B.spSeq = nullptr; }
+  return C;
+}
+}  // namespace detail
+
+// ParFriends.h:798-800 signature
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2, typename UDERA,
+          typename UDERB>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_DoubleBuff(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B,
+                                                bool clearA = false, bool clearB = false, int exec = CBG_EXEC_PANEL) {
+  return detail::summa<SR, NUO, UDERO>(A, B, CBG_DOUBLEBUFF, clearA, clearB, exec);
+}
+// ParFriends.h:1004-1006 signature
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2, typename UDERA,
+          typename UDERB>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B,
+                                           bool clearA = false, bool clearB = false, int exec = CBG_EXEC_PANEL) {
+  return detail::summa<SR, NUO, UDERO>(A, B, CBG_SYNCH, clearA, clearB, exec);
+}
+// SpParMat.h:454-467
+template <typename SR, typename IU, typename NU1, typename NU2, typename UDERA, typename UDERB>
+SpParMat<IU, typename SR::T_promote, UDERA> PSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B) {
+  return Mult_AnXBn_Synch<SR, typename SR::T_promote, UDERA>(A, B);
+}
+
+}  // namespace combblas_amd
