@@ -99,12 +99,15 @@ def main():
 
         grid = cbg.CommGrid(0, 1, transport="host", host_comm=Self())
     else:
-        import torch.distributed as dist  # bootstrap only (gloo, host side)
-        dist.init_process_group("gloo")
-        uid = [cbg.CommGrid.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        # Host rendezvous for the RCCL unique id over plain TCP (MASTER_PORT+1):
+        # the GPU processes never import torch, whose ROCm wheel would load a
+        # second HIP runtime into the process.
         pr, pc = GRIDS[N]
-        grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid[0], transport="rccl")
+        hc = cbg.TcpHostComm(rank, N, pr, pc, os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                             int(os.environ.get("MASTER_PORT", "29500")) + 1)
+        uid = hc.bcast_object(cbg.CommGrid.unique_id() if rank == 0 else None, root=0)
+        hc.close()
+        grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid, transport="rccl")
 
     t_gen = time.perf_counter()
     A = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)

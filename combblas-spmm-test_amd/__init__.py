@@ -400,6 +400,113 @@ class GlooHostComm:
         return b"".join(o.numpy().tobytes() for o in out)
 
 
+class TcpHostComm:
+    """Host transport over plain TCP sockets (rank 0 is the hub), no torch.
+
+    The GPU processes must not import torch: torch's ROCm wheel carries its own
+    HIP runtime, and a second runtime in the process corrupts the heap at exit.
+    Every collective is world-synchronous (row and column communicators
+    partition the world): each rank sends its payload to the hub, which replies
+    with what that rank must receive.  Used for the RCCL unique-id rendezvous of
+    bench.py and for multi-process tests on one GPU.
+    """
+
+    def __init__(self, rank, world, grid_rows=1, grid_cols=None, addr="127.0.0.1", port=29511, timeout=120.0):
+        import socket
+        import struct
+        import time
+        self._struct = struct
+        self.rank, self.world = rank, world
+        self.pr = grid_rows
+        self.pc = grid_cols if grid_cols is not None else world // grid_rows
+        self.prow, self.pcol = rank // self.pc, rank % self.pc
+        self.peers = {}
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world)
+            srv.settimeout(timeout)
+            while len(self.peers) < world - 1:
+                c, _ = srv.accept()
+                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                r = struct.unpack("<q", self._recv(c, 8))[0]
+                self.peers[r] = c
+            srv.close()
+        else:
+            t0 = time.time()
+            while True:
+                try:
+                    c = socket.create_connection((addr, port), timeout=timeout)
+                    break
+                except OSError:
+                    if time.time() - t0 > timeout:
+                        raise
+                    time.sleep(0.05)
+            c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            c.sendall(struct.pack("<q", rank))
+            self.hub = c
+
+    @staticmethod
+    def _recv(c, n):
+        buf = bytearray(n)
+        mv = memoryview(buf)
+        got = 0
+        while got < n:
+            k = c.recv_into(mv[got:], n - got)
+            if k == 0:
+                raise ConnectionError("peer closed")
+            got += k
+        return bytes(buf)
+
+    def _send_msg(self, c, b):
+        c.sendall(self._struct.pack("<q", len(b)) + b)
+
+    def _recv_msg(self, c):
+        n = self._struct.unpack("<q", self._recv(c, 8))[0]
+        return self._recv(c, n)
+
+    def _members(self, comm, r):
+        pr_, pc_ = r // self.pc, r % self.pc
+        if comm == 1:
+            return [pr_ * self.pc + c for c in range(self.pc)]
+        if comm == 2:
+            return [q * self.pc + pc_ for q in range(self.pr)]
+        return list(range(self.world))
+
+    def _exchange(self, payload, reply_fn):
+        if self.world == 1:
+            return reply_fn({0: payload}, 0)
+        if self.rank != 0:
+            self._send_msg(self.hub, payload)
+            return self._recv_msg(self.hub)
+        got = {0: payload}
+        for r, c in self.peers.items():
+            got[r] = self._recv_msg(c)
+        for r, c in self.peers.items():
+            self._send_msg(c, reply_fn(got, r))
+        return reply_fn(got, 0)
+
+    def bcast(self, comm, arr, root):
+        mine = bytes(arr) if self._members(comm, self.rank)[root] == self.rank else b""
+        res = self._exchange(mine, lambda got, r: got[self._members(comm, r)[root]])
+        arr[:] = memoryview(res).cast("B")
+
+    def allgather(self, comm, data):
+        return self._exchange(bytes(data), lambda got, r: b"".join(got[q] for q in self._members(comm, r)))
+
+    def bcast_object(self, obj, root=0):
+        import pickle
+        res = self._exchange(pickle.dumps(obj) if self.rank == root else b"", lambda got, r: got[root])
+        return pickle.loads(res)
+
+    def close(self):
+        for c in getattr(self, "peers", {}).values():
+            c.close()
+        if hasattr(self, "hub"):
+            self.hub.close()
+
+
 def block_range(total, parts, idx):
     """Block distribution of SpParMat::Owner (SpParMat.cpp:5068-5097): last block takes the remainder."""
     per = total // parts

@@ -26,13 +26,24 @@ def add_digests(ds):
 def main():
     mode, pr, pc, case = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     cbg = load_cbg()
-    if mode == "gpu":
-        cbg.lib()
-    import torch.distributed as dist
-    dist.init_process_group("gloo")
-    rank, world = dist.get_rank(), dist.get_world_size()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     assert world == pr * pc
-    hc = cbg.GlooHostComm(pr, pc)
+    port = int(os.environ["MASTER_PORT"]) + 1
+    if mode == "gpu" or mode == "cputcp":
+        # GPU processes never import torch (a second HIP runtime corrupts the heap)
+        if mode == "gpu":
+            cbg.lib()
+        hc = cbg.TcpHostComm(rank, world, pr, pc, "127.0.0.1", port)
+
+        class _D:
+            @staticmethod
+            def barrier():
+                hc.allgather(0, b"x")
+        dist = _D
+    else:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        hc = cbg.GlooHostComm(pr, pc)
     G = golden()
     if case.startswith("rmat"):
         A = load_npz("rmat_s10_ef16_A.npz")
@@ -42,7 +53,7 @@ def main():
         A = load_npz("largeseq_A.npz")
         B = load_npz("largeseq_B.npz")
         gd = G["files"]["largeseq"]["C_local_plus"]
-    if mode == "cpu":
+    if mode in ("cpu", "cputcp"):
         # tiles of the block distribution cover A exactly once
         r0, r1 = cbg.block_range(A["m"], pr, hc.prow)
         c0, c1 = cbg.block_range(A["n"], pc, hc.pcol)

@@ -33,8 +33,10 @@ def launch(nproc, args, timeout=300):
 
 @pytest.mark.parametrize("grid", [(1, 2), (2, 1), (2, 2)])
 @pytest.mark.parametrize("case", ["rmat", "largeseq"])
-def test_host_transport_cpu(grid, case):
-    rc, out = launch(grid[0] * grid[1], ["cpu", str(grid[0]), str(grid[1]), case])
+@pytest.mark.parametrize("transport", ["cpu", "cputcp"])
+def test_host_transport_cpu(grid, case, transport):
+    """gloo (GlooHostComm) and plain-TCP (TcpHostComm) transports: same collectives, same answers."""
+    rc, out = launch(grid[0] * grid[1], [transport, str(grid[0]), str(grid[1]), case])
     assert rc == 0 and "MPOK" in out, out[-3000:]
 
 
