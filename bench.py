@@ -87,7 +87,7 @@ def main():
     N = max(world, 1)
     scale = a.scale if a.scale is not None else (18 if N == 1 else 22)
     cbg = load_cbg()  # libcbg first: its HIP/RCCL runtimes are the ones the process uses
-    cbg.lib().cbg_set_device(local_rank)
+    cbg.lib().cbg_set_device(local_rank % max(1, cbg.device_count()))
 
     if N == 1:
         class Self:
@@ -98,6 +98,7 @@ def main():
                 return data
 
         grid = cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+        transport = "none"
     else:
         # Host rendezvous for the RCCL unique id over plain TCP (MASTER_PORT+1):
         # the GPU processes never import torch, whose ROCm wheel would load a
@@ -106,8 +107,18 @@ def main():
         hc = cbg.TcpHostComm(rank, N, pr, pc, os.environ.get("MASTER_ADDR", "127.0.0.1"),
                              int(os.environ.get("MASTER_PORT", "29500")) + 1)
         uid = hc.bcast_object(cbg.CommGrid.unique_id() if rank == 0 else None, root=0)
-        hc.close()
-        grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid, transport="rccl")
+        try:
+            grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid, transport="rccl")
+            transport = "rccl"
+            hc.close()
+        except cbg.CbgError as e:
+            # e.g. several ranks on one GPU (RCCL rejects duplicate devices): keep
+            # the SUMMA on the host transport so the run still completes
+            print(f"[bench] rank {rank}: RCCL grid unavailable ({e}); using the TCP host transport",
+                  file=sys.stderr, flush=True)
+            hc.allgather(0, b"0")  # every rank agrees on the fallback
+            grid = cbg.CommGrid(rank, N, pr, pc, transport="host", host_comm=hc)
+            transport = "host-tcp"
 
     t_gen = time.perf_counter()
     A = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)
@@ -163,7 +174,7 @@ def main():
                 scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
-                "big_columns": st["n_big"], "slabs": st["n_slabs"]},
+                "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
