@@ -211,6 +211,65 @@ __device__ __forceinline__ void bitonic_sort_kv(int* keys, double* vals, int tid
   }
 }
 
+// Emit the n occupied slots of an LDS hash table (keys[T], vals[T]; empty =
+// EMPTY_KEY) in ascending key order to out[obase ...] without a full sort:
+// keys are bucketed by (key - lo) >> bshift into NB buckets (counting sort),
+// and each entry's position inside its bucket is its rank among the few
+// entries of that bucket.  O(T + n * bucket size) work, 3 barriers.
+// Scratch: boff[NB+1], cur[NB] ints, members[n] (slot ids).
+template <int T, int BS, int NB>
+__device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* vals, int lo, int bshift, int* boff,
+                                                 int* cur, unsigned short* members, int* tmp,
+                                                 int32_t* __restrict__ out_ir, double* __restrict__ out_val,
+                                                 int64_t obase) {
+  const int tid = threadIdx.x;
+  for (int b = tid; b < NB; b += BS) cur[b] = 0;
+  __syncthreads();
+  for (int j = tid; j < T; j += BS) {
+    const int k = keys[j];
+    if (k != EMPTY_KEY) atomicAdd(&cur[(k - lo) >> bshift], 1);
+  }
+  __syncthreads();
+  // exclusive scan of the bucket counts (NB/BS per thread)
+  constexpr int BPT = (NB + BS - 1) / BS;
+  int c[BPT];
+  int sum = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int b = tid * BPT + q;
+    c[q] = (b < NB) ? cur[b] : 0;
+    sum += c[q];
+  }
+  int total;
+  int run = block_excl_scan<BS>(sum, tmp, &total);
+#pragma unroll
+  for (int q = 0; q < BPT; ++q) {
+    const int b = tid * BPT + q;
+    if (b < NB) {
+      boff[b] = run;
+      cur[b] = run;
+    }
+    run += c[q];
+  }
+  if (tid == 0) boff[NB] = total;
+  __syncthreads();
+  for (int j = tid; j < T; j += BS) {
+    const int k = keys[j];
+    if (k != EMPTY_KEY) members[atomicAdd(&cur[(k - lo) >> bshift], 1)] = (unsigned short)j;
+  }
+  __syncthreads();
+  for (int p = tid; p < total; p += BS) {
+    const int j = members[p];
+    const int k = keys[j];
+    const int b = (k - lo) >> bshift;
+    int r = boff[b];
+    const int e = boff[b + 1];
+    for (int q = boff[b]; q < e; ++q) r += keys[members[q]] < k;
+    out_ir[obase + r] = k;
+    out_val[obase + r] = vals[j];
+  }
+}
+
 struct WaveSync {
   __device__ __forceinline__ void operator()() const { wave_sync(); }
 };

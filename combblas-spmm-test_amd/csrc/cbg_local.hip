@@ -22,6 +22,8 @@
 // staged in LDS with a prefix sum of A-column lengths, and consecutive lanes
 // take consecutive products, so reads of A's columns are coalesced whatever
 // their length (R-MAT hub columns included).
+#include <cstring>
+
 #include "cbg_device.h"
 #include "cbg_internal.h"
 
@@ -31,6 +33,15 @@ namespace cbg {
 //   1: k_sym_panel skips its product loop     2: k_num_slab skips pass 0 products
 //   4: k_num_slab skips pass 1 products       8: k_num_slab skips the output writes
 __constant__ int c_dbg;
+//   16: k_num_slab accumulates per-phase wall time (thread 0 of every block) into g_phase
+__device__ unsigned long long g_phase[16];
+__device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
+  if ((c_dbg & 16) && threadIdx.x == 0) {
+    const unsigned long long n = wall_clock64();
+    atomicAdd(&g_phase[k], n - t);
+    t = n;
+  }
+}
 
 // ----------------------------------------------------------------------------
 // small kernels
@@ -250,6 +261,8 @@ constexpr int PANEL_LOG_MAX = 18;       // max rows of a panel (LDS bitmap, 32 K
 constexpr int SLAB_WORDS = 1 << (PANEL_LOG_MAX - 5);
 constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= max slabs) per panel
 constexpr int BIG_BS = 512;
+constexpr int SPARSE_SLAB_MAX = 4096;   // products of a (column, panel) pair counted by hash -> hash slab
+constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 
 // cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r
 __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
@@ -290,12 +303,70 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), m);
   const int words = (R1 - R0 + 31) >> 5;
   const int2* cm = cmapP + (int64_t)r * nA1;
+  const int64_t p0 = cpB[col], p1 = cpB[col + 1];
+  if (p1 - p0 <= BS) {
+    // single chunk: stage once; a pair with few products is counted with an
+    // LDS hash sized to it and becomes ONE sparse (hash) slab -- its cost then
+    // scales with its products, not with the panel's 2^plog rows
+    const int64_t p = p0 + tid;
+    int s = 0, len = 0;
+    if (p < p1) {
+      const int2 e = cm[irB[p]];
+      s = e.x;
+      len = e.y - e.x;
+    }
+    int total;
+    const int ex = block_excl_scan<BS>(len, tmp, &total);
+    pref[tid] = ex;
+    if (tid == BS - 1) pref[BS] = total;
+    st[tid] = s;
+    int T = 512;
+    while (T < 2 * total) T <<= 1;
+    if (total <= SPARSE_SLAB_MAX && T <= pwords) {
+      int* keys = reinterpret_cast<int*>(bm);
+      for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
+      __syncthreads();
+      int count = 0;
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          [&](const SegI& g, int u) { return irA[g.off + u]; },
+          [&](int row) {
+            unsigned h = ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1);
+            while (true) {
+              const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+              if (old == EMPTY_KEY) { ++count; break; }
+              if (old == row) break;
+              h = (h + 1) & (unsigned)(T - 1);
+            }
+          });
+      count = wave_sum(count);
+      if (tid == 0) fine[0] = 0;
+      __syncthreads();
+      if (lane_id() == 0 && count) atomicAdd(&fine[0], count);
+      __syncthreads();
+      if (tid == 0) {
+        const int cnt_pair = fine[0];
+        nslab[br] = cnt_pair ? 1 : 0;
+        if (cnt_pair) desc[(int64_t)br * NFINE_MAX] = make_int4(R0, R1, 0, cnt_pair | SLAB_SPARSE);
+        cnt_br[br] = cnt_pair;
+        if (cnt_pair) atomicAdd(&cnt[col], cnt_pair);
+      }
+      return;
+    }
+    for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
+    if (tid < NFINE_MAX) fine[tid] = 0;
+    __syncthreads();
+    if (!(c_dbg & 1))
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
+          [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
+    __syncthreads();
+  } else {
   for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
   if (tid < NFINE_MAX) fine[tid] = 0;
   __syncthreads();
-  const int64_t p0 = cpB[col], p1 = cpB[col + 1];
-  for (int64_t c0 = p0; c0 < p1; c0 += BS) {
-    const int64_t p = c0 + tid;
+  for (int64_t c0 = p0; c0 < p1; c0 += BS) {    const int64_t p = c0 + tid;
     int s = 0, len = 0;
     if (p < p1) {
       const int2 e = cm[irB[p]];
@@ -314,6 +385,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
           [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
     __syncthreads();
+  }
   }
   // per fine range popcounts: thread t owns WPT consecutive words inside one
   // fine range (256 words); G lanes share a fine range and reduce by shuffles
@@ -359,16 +431,26 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   }
 }
 
-// slab work lists per launch class (small: nnz <= small_cap); turns the
-// within-panel offsets of the slab plan into within-column offsets
-__global__ void k_slab_list(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
-                            int4* __restrict__ desc, int small_cap, int2* __restrict__ small_list,
-                            int2* __restrict__ large_list, int* __restrict__ counters) {
-  __shared__ int lc[2], lb[2];
-  if (threadIdx.x < 2) lc[threadIdx.x] = 0;
+// slab work lists per launch class.  Classes: 0 bitmap small (nnz <=
+// small_cap), 1 bitmap large, 2+k hash slab with table 2^(SLAB_HASH_LOG0+k).
+constexpr int SLAB_HASH_LOG0 = 9, SLAB_HASH_NCLS = 5;  // tables 512 .. 8192
+constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS;
+__device__ __forceinline__ int slab_class(int w, int small_cap) {
+  if (w & SLAB_SPARSE) {
+    const int c = w & (SLAB_SPARSE - 1);
+    int k = 0;
+    while ((1 << (SLAB_HASH_LOG0 + k)) < 2 * c) ++k;
+    return 2 + k;
+  }
+  return w <= small_cap ? 0 : 1;
+}
+// pass 1: within-panel -> within-column offsets, class counts
+__global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
+                             int4* __restrict__ desc, int small_cap, int* __restrict__ counts) {
+  __shared__ int lc[SLAB_NCLS];
+  if (threadIdx.x < SLAB_NCLS) lc[threadIdx.x] = 0;
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  int nsm = 0, nl = 0;
   if (b < nbig) {
     int off = 0;
     for (int r = 0; r < R; ++r) {
@@ -376,22 +458,59 @@ __global__ void k_slab_list(int nbig, int R, const int32_t* __restrict__ nslab, 
       for (int s = 0; s < nslab[br]; ++s) {
         int4& d = desc[(int64_t)br * NFINE_MAX + s];
         d.z += off;
-        if (d.w <= small_cap) ++nsm; else ++nl;
+        atomicAdd(&lc[slab_class(d.w, small_cap)], 1);
       }
       off += cnt_br[br];
     }
   }
-  const int o0 = atomicAdd(&lc[0], nsm), o1 = atomicAdd(&lc[1], nl);
   __syncthreads();
-  if (threadIdx.x < 2) lb[threadIdx.x] = atomicAdd(&counters[threadIdx.x], lc[threadIdx.x]);
+  if (threadIdx.x < SLAB_NCLS && lc[threadIdx.x]) atomicAdd(&counts[threadIdx.x], lc[threadIdx.x]);
+}
+// class bases (exclusive prefix of the counts) into cursor[]
+__global__ void k_slab_bases(const int* __restrict__ counts, int* __restrict__ cursor) {
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int c = 0; c < SLAB_NCLS; ++c) {
+      cursor[c] = s;
+      s += counts[c];
+    }
+  }
+}
+// pass 2: (pair, slab) entries into their class segment of one list
+__global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, const int4* __restrict__ desc,
+                            int small_cap, int* __restrict__ cursor, int2* __restrict__ list) {
+  __shared__ int lc[SLAB_NCLS], lb[SLAB_NCLS];
+  if (threadIdx.x < SLAB_NCLS) lc[threadIdx.x] = 0;
+  __syncthreads();
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  int mine[SLAB_NCLS];
+#pragma unroll
+  for (int c = 0; c < SLAB_NCLS; ++c) mine[c] = 0;
+  if (b < nbig)
+    for (int r = 0; r < R; ++r) {
+      const int br = b * R + r;
+      for (int s = 0; s < nslab[br]; ++s) {
+        const int c = slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap);
+#pragma unroll
+        for (int q = 0; q < SLAB_NCLS; ++q) mine[q] += (q == c);
+      }
+    }
+  int o[SLAB_NCLS];
+#pragma unroll
+  for (int c = 0; c < SLAB_NCLS; ++c) o[c] = mine[c] ? atomicAdd(&lc[c], mine[c]) : 0;
+  __syncthreads();
+  if (threadIdx.x < SLAB_NCLS && lc[threadIdx.x]) lb[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], lc[threadIdx.x]);
   __syncthreads();
   if (b >= nbig) return;
-  int a0 = lb[0] + o0, a1 = lb[1] + o1;
+#pragma unroll
+  for (int c = 0; c < SLAB_NCLS; ++c) o[c] += lb[c];
   for (int r = 0; r < R; ++r) {
     const int br = b * R + r;
     for (int s = 0; s < nslab[br]; ++s) {
-      if (desc[(int64_t)br * NFINE_MAX + s].w <= small_cap) small_list[a0++] = make_int2(br, s);
-      else large_list[a1++] = make_int2(br, s);
+      const int c = slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap);
+#pragma unroll
+      for (int q = 0; q < SLAB_NCLS; ++q)
+        if (q == c) list[o[q]++] = make_int2(br, s);
     }
   }
 }
@@ -466,7 +585,9 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
 template <int LOGT, int BS>
 struct NumBlockLds {
   static constexpr int T = 1 << LOGT;
-  static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4;
+  static constexpr int NB = 1024;  // buckets of the sorted emit
+  static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
+                               (2 * NB + 4) * 4 + (T / 2) * 2;
 };
 
 template <int LOGT, int BS, int SR>
@@ -474,7 +595,8 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
                                                   const int32_t* __restrict__ irB, const double* __restrict__ valB,
                                                   const int2* __restrict__ cmap, const int32_t* __restrict__ irA,
                                                   const double* __restrict__ valA, const int64_t* __restrict__ colptr,
-                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
+                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val,
+                                                  int bshift) {
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);
@@ -514,13 +636,11 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
         [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     __syncthreads();
   }
-  bitonic_sort_kv<T, BS>(keys, vals, tid, BlockSync());
-  const int64_t o = colptr[col];
-  const int nout = (int)(colptr[col + 1] - o);
-  for (int e = tid; e < nout; e += BS) {
-    out_ir[o + e] = keys[e];
-    out_val[o + e] = vals[e];
-  }
+  constexpr int NB = NumBlockLds<LOGT, BS>::NB;
+  int* boff = tmp + BS / WAVE + 4;
+  int* cur = boff + NB + 4;
+  unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
+  hash_emit_sorted<T, BS, NB>(keys, vals, 0, bshift, boff, cur, members, tmp, out_ir, out_val, colptr[col]);
 }
 
 // numeric: one row slab of a big column by bitmap + rank.
@@ -589,6 +709,7 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   const int words = (hi - lo + 31) >> 5;
   const int64_t obase = colptr[col] + d.z;
   const bool full_range = (lo == R0) && (hi == R1);  // the slab is the whole panel
+  unsigned long long tmark = wall_clock64();
   const bool have_bm = gbm != nullptr;  // bitmap kept by the symbolic phase: no marking pass
   if (have_bm) {
     const unsigned* src = gbm + (int64_t)e.x * SLAB_WORDS + ((lo - R0) >> 5);
@@ -598,6 +719,7 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   }
   for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
   __syncthreads();
+  phase_mark(tmark, 0);
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
   const bool one_chunk = (p1 - p0) <= BS;
   const int first_pass = have_bm ? 1 : 0;
@@ -622,6 +744,7 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
         run += c[k];
       }
       __syncthreads();
+      phase_mark(tmark, 3);
     }
     for (int64_t c0 = p0; c0 < p1; c0 += BS) {
       int total;
@@ -648,11 +771,13 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
         st[tid] = s;
         bv[tid] = bval;
         __syncthreads();
+        phase_mark(tmark, 1);
       } else {
         total = pref[BS];  // staging of the single chunk is reused by pass 1
       }
       if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
       __syncthreads();
+      phase_mark(tmark, 4 + pass);
     }
   }
   // rows: each word emits its set bits at their ranks; values: coalesced copy
@@ -668,6 +793,82 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
     }
   }
   for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
+  if (c_dbg & 16) {
+    __syncthreads();
+    phase_mark(tmark, 6);
+  }
+}
+
+// numeric of a sparse (column, panel) pair (hash-mode slab, <= SPARSE_SLAB_MAX
+// products): LDS hash sized to the pair's nnz, sorted emit by row buckets
+template <int LOGT, int BS>
+struct SlabHashLds {
+  static constexpr int T = 1 << LOGT;
+  static constexpr int NB = T / 4;  // row buckets of the sorted emit
+  // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[T/2] u16
+  static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
+                               (2 * NB + 4) * 4 + (T / 2) * 2;
+};
+
+template <int SR, int LOGT, int BS>
+__global__ __launch_bounds__(BS) void k_num_slab_hash(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
+                                                      const int4* __restrict__ desc, int R, int plog,
+                                                      const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                      const double* __restrict__ valB, const int2* __restrict__ cmapP,
+                                                      int64_t nA1, const int32_t* __restrict__ irA,
+                                                      const double* __restrict__ valA,
+                                                      const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
+                                                      double* __restrict__ out_val) {
+  using L = SlabHashLds<LOGT, BS>;
+  constexpr int T = L::T, NB = L::NB;
+  constexpr int LOGNB = LOGT - 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* vals = reinterpret_cast<double*>(smem);
+  double* bv = vals + T;
+  int* keys = reinterpret_cast<int*>(bv + BS);
+  int* pref = keys + T;
+  int* st = pref + BS + 4;
+  int* tmp = st + BS;
+  int* boff = tmp + BS / WAVE + 4;
+  int* cur = boff + NB + 4;
+  unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
+  const int tid = threadIdx.x;
+  const int2 e = list[blockIdx.x];
+  const int4 d = desc[(int64_t)e.x * NFINE_MAX + e.y];
+  const int col = perm_big[e.x / R];
+  const int r = e.x % R;
+  const int2* cm = cmapP + (int64_t)r * nA1;
+  for (int j = tid; j < T; j += BS) {
+    keys[j] = EMPTY_KEY;
+    vals[j] = Sem<SR>::identity();
+  }
+  __syncthreads();
+  const int64_t p1 = cpB[col + 1];
+  for (int64_t c0 = cpB[col]; c0 < p1; c0 += BS) {
+    const int64_t p = c0 + tid;
+    int s = 0, len = 0;
+    double bval = 0.0;
+    if (p < p1) {
+      const int2 ce = cm[irB[p]];
+      s = ce.x;
+      len = ce.y - ce.x;
+      bval = valB[p];
+    }
+    int total;
+    const int ex = block_excl_scan<BS>(len, tmp, &total);
+    pref[tid] = ex;
+    if (tid == BS - 1) pref[BS] = total;
+    st[tid] = s;
+    bv[tid] = bval;
+    __syncthreads();
+    block_products<BS>(
+        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
+    __syncthreads();
+  }
+  const int bshift = plog > LOGNB ? plog - LOGNB : 0;
+  hash_emit_sorted<T, BS, NB>(keys, vals, d.x, bshift, boff, cur, members, tmp, out_ir, out_val, colptr[col] + d.z);
 }
 
 // ----------------------------------------------------------------------------
@@ -708,9 +909,9 @@ static const int64_t kSymThr[] = {0, 32, 128, 512, 1024, 2048, 4096};
 // nnz fits the largest numeric hash bin
 static int64_t big_flops(int64_t m) {
   static const char* e = getenv("CBG_BIG_FLOPS");
-  // a (column, panel) bitmap costs ~P/32 words of fixed LDS work; measured on
-  // R-MAT: 1024 best at m = 2^18 (one panel), 2048 at m = 2^20 (four panels)
-  int64_t b = e ? atoll(e) : (m <= (1LL << 18) ? 1024 : 2048);
+  // measured on R-MAT (scale 18/20): 4096 once hash slabs take the sparse
+  // (column, panel) pairs and the block hash bins emit by bucket sort
+  int64_t b = e ? atoll(e) : 4096;
   if (b < 64) b = 64;
   if (b > 4096) b = 4096;
   return b;
@@ -751,8 +952,11 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
   if (n <= 0) return;
   const size_t lds = NumBlockLds<LOGT, BS>::BYTES;
   set_lds(k_num_block<LOGT, BS, SR>, lds);
+  int lm = 0;
+  while ((1LL << lm) < A.m) ++lm;
+  const int bshift = std::max(0, lm - 10);  // NumBlockLds::NB = 2^10 buckets over [0, m)
   hipLaunchKernelGGL((k_num_block<LOGT, BS, SR>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, B.val, cmap, A.ir,
-                     A.val, colptr, C.ir, C.val);
+                     A.val, colptr, C.ir, C.val, bshift);
 }
 
 struct BigPlan {
@@ -764,25 +968,49 @@ struct BigPlan {
   DBuf<unsigned> gbm;
 };
 
+template <int SR, int LOGT, int BS>
+static void launch_slab_hash(const int2* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                             const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+  if (n <= 0) return;
+  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
+  auto k = k_num_slab_hash<SR, LOGT, BS>;
+  set_lds(k, L);
+  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.perm_big, bp.desc.p, bp.R, bp.plog, B.cp, B.ir,
+                     B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val);
+}
+
+// ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 template <int SR>
-static void launch_slabs(const int2* small, int nsmall, const int2* large, int nlarge, const BigPlan& bp,
-                         const cbg_tile& A, const cbg_tile& B, const int64_t* colptr, cbg_tile& C, hipStream_t s) {
-  if (nsmall > 0) {
+static void launch_slabs(const int2* list, const int* ncls, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                         const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+  const int2* at[SLAB_NCLS];
+  int64_t o = 0;
+  for (int c = 0; c < SLAB_NCLS; ++c) {
+    at[c] = list + o;
+    o += ncls[c];
+  }
+  if (ncls[0] > 0) {
     constexpr int L = SlabLds<SLAB_SMALL_CAP, SLAB_SMALL_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>;
     set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)nsmall), dim3(SLAB_SMALL_BS), L, s, small, bp.perm_big, bp.desc.p, bp.R,
+    hipLaunchKernelGGL(k, dim3((unsigned)ncls[0]), dim3(SLAB_SMALL_BS), L, s, at[0], bp.perm_big, bp.desc.p, bp.R,
                        bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
                        bp.gbm.p);
   }
-  if (nlarge > 0) {
+  if (ncls[1] > 0) {
     constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
     auto k = k_num_slab<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>;
     set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)nlarge), dim3(SLAB_LARGE_BS), L, s, large, bp.perm_big, bp.desc.p, bp.R,
+    hipLaunchKernelGGL(k, dim3((unsigned)ncls[1]), dim3(SLAB_LARGE_BS), L, s, at[1], bp.perm_big, bp.desc.p, bp.R,
                        bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
                        bp.gbm.p);
   }
+  static_assert(SLAB_HASH_LOG0 == 9 && SLAB_HASH_NCLS == 5, "hash slab classes");
+  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, colptr, C, s);
+  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, colptr, C, s);
+  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, colptr, C, s);
+  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, colptr, C, s);
+  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, colptr, C, s);
 }
 
 static double bitmap_budget_bytes() {
@@ -936,7 +1164,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipMemcpyAsync(&nnzc, colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   // slab lists of big columns
   DBuf<int64_t> sbase;
-  DBuf<int2> slist, slarge;
+  DBuf<int2> slist;
   int64_t nslabs = 0;
   if (nbig > 0) {
     sbase.reset(nbr + 1);
@@ -945,15 +1173,17 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));
-  int ncls[2] = {0, 0};
+  int ncls[SLAB_NCLS] = {};
   if (nbig > 0 && nslabs > 0) {
     slist.reset(nslabs);
-    slarge.reset(nslabs);
-    DBuf<int> counters(2);
-    CBG_HIP(hipMemsetAsync(counters.p, 0, 2 * sizeof(int), s));
-    hipLaunchKernelGGL(k_slab_list, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.cnt_br.p,
-                       bp.desc.p, SLAB_SMALL_CAP, slist.p, slarge.p, counters.p);
-    CBG_HIP(hipMemcpyAsync(ncls, counters.p, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    DBuf<int> counters(2 * SLAB_NCLS);
+    CBG_HIP(hipMemsetAsync(counters.p, 0, 2 * SLAB_NCLS * sizeof(int), s));
+    hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.cnt_br.p,
+                       bp.desc.p, SLAB_SMALL_CAP, counters.p);
+    hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, counters.p, counters.p + SLAB_NCLS);
+    hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.desc.p,
+                       SLAB_SMALL_CAP, counters.p + SLAB_NCLS, slist.p);
+    CBG_HIP(hipMemcpyAsync(ncls, counters.p, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));
   }
   // output arrays
@@ -966,8 +1196,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls[0], slarge.p, ncls[1], bp, A, B, colptr.p, C, s);
-    else launch_slabs<0>(slist.p, ncls[0], slarge.p, ncls[1], bp, A, B, colptr.p, C, s);
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, colptr.p, C, s);
+    else launch_slabs<0>(slist.p, ncls, bp, A, B, colptr.p, C, s);
   }
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
@@ -984,6 +1214,20 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipEventRecord(ev2, s));
   CBG_HIP(hipStreamSynchronize(s));
   CBG_HIP(hipGetLastError());
+  {
+    static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
+    if (dbg & 16) {
+      unsigned long long ph[16];
+      CBG_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph)));
+      const char* names[7] = {"init", "staging", "-", "rankscan", "pass0", "pass1", "output"};
+      std::fprintf(stderr, "[cbg phases, block-us summed / 256 CUs]");
+      for (int k = 0; k < 7; ++k)
+        if (k != 2) std::fprintf(stderr, " %s=%.3fms", names[k], ph[k] / 100.0 / 256.0 / 1000.0);
+      std::fprintf(stderr, "\n");
+      std::memset(ph, 0, sizeof(ph));
+      CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph)));
+    }
+  }
   if (st) {
     float a = 0, b = 0;
     CBG_HIP(hipEventElapsedTime(&a, ev0, ev1));
