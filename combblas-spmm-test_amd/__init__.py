@@ -30,7 +30,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcbg.so")
+# CBG_LIB: alternative build of libcbg (tuning experiments: tools/variants.sh)
+LIB_PATH = os.environ.get("CBG_LIB") or os.path.join(_HERE, "libcbg.so")
 
 PLUS_TIMES, MIN_PLUS = 0, 1
 DOUBLEBUFF, SYNCH = 0, 1

@@ -8,6 +8,9 @@
 namespace cbg {
 
 constexpr int WAVE = 64;
+#ifndef CBG_PRODUCTS_U
+#define CBG_PRODUCTS_U 4  // products in flight per lane in wave_products (2 or 4)
+#endif
 constexpr int EMPTY_KEY = 0x7FFFFFFF;  // empty hash slot; sorts after every row id
 
 // Order LDS traffic between the lanes of ONE wave (LDS executes a wave's
@@ -75,6 +78,44 @@ __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
   return r;
 }
 
+// Block-wide exclusive scan of get(i), i in [0, n), in index order: put(i, prefix)
+// for every i; returns the total.  Wave w owns a contiguous span of indices and
+// its lanes take consecutive ones (conflict-free LDS access for array-backed
+// get/put, unlike a per-thread contiguous chunk).  get() is called twice per
+// index.  tmp holds >= BS/64+1 ints.  Contains barriers.
+template <int BS, class G, class P>
+__device__ __forceinline__ int block_ordered_scan(int n, G&& get, P&& put, int* tmp) {
+  constexpr int NW = BS / WAVE;
+  const int lane = lane_id(), w = threadIdx.x / WAVE;
+  const int span = ((n + BS - 1) / BS) * WAVE;
+  const int b0 = min(w * span, n), b1 = min(b0 + span, n);
+  int tot = 0;
+  for (int i = b0 + lane; i - lane < b1; i += WAVE) tot += (i < b1) ? get(i) : 0;
+  tot = wave_sum(tot);
+  if (lane == 0) tmp[w] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int q = 0; q < NW; ++q) {
+      const int t = tmp[q];
+      tmp[q] = s;
+      s += t;
+    }
+    tmp[NW] = s;
+  }
+  __syncthreads();
+  int run = tmp[w];
+  for (int i = b0 + lane; i - lane < b1; i += WAVE) {
+    const int c = (i < b1) ? get(i) : 0;
+    const int incl = wave_incl_scan(c);
+    if (i < b1) put(i, run + incl - c);
+    run += __shfl(incl, WAVE - 1, WAVE);
+  }
+  const int total = tmp[NW];
+  __syncthreads();
+  return total;
+}
+
 // largest i in [0, n) with pref[i] <= u, for a non-decreasing pref[0..n] with pref[0] = 0 <= u
 __device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
   int lo = 0, hi = n;  // invariant: pref[lo] <= u < pref[hi]
@@ -103,6 +144,37 @@ __device__ __forceinline__ void wave_products(const int* pref, int nseg, int u0,
   int sg = seg_search(pref, nseg, u);
   int nxt = pref[sg + 1];
   auto cur = seg(sg);
+#if CBG_PRODUCTS_U == 4
+  for (; u + 3 * WAVE < u1; u += 4 * WAVE) {
+    if (u >= nxt) {
+      do nxt = pref[++sg + 1]; while (u >= nxt);
+      cur = seg(sg);
+    }
+    auto x0 = load(cur, u);
+    int v = u + WAVE;
+    if (v >= nxt) {
+      do nxt = pref[++sg + 1]; while (v >= nxt);
+      cur = seg(sg);
+    }
+    auto x1 = load(cur, v);
+    v += WAVE;
+    if (v >= nxt) {
+      do nxt = pref[++sg + 1]; while (v >= nxt);
+      cur = seg(sg);
+    }
+    auto x2 = load(cur, v);
+    v += WAVE;
+    if (v >= nxt) {
+      do nxt = pref[++sg + 1]; while (v >= nxt);
+      cur = seg(sg);
+    }
+    auto x3 = load(cur, v);
+    apply(x0);
+    apply(x1);
+    apply(x2);
+    apply(x3);
+  }
+#endif
   for (; u + WAVE < u1; u += 2 * WAVE) {
     if (u >= nxt) {
       do nxt = pref[++sg + 1]; while (u >= nxt);
@@ -230,27 +302,14 @@ __device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* 
     if (k != EMPTY_KEY) atomicAdd(&cur[(k - lo) >> bshift], 1);
   }
   __syncthreads();
-  // exclusive scan of the bucket counts (NB/BS per thread)
-  constexpr int BPT = (NB + BS - 1) / BS;
-  int c[BPT];
-  int sum = 0;
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int b = tid * BPT + q;
-    c[q] = (b < NB) ? cur[b] : 0;
-    sum += c[q];
-  }
-  int total;
-  int run = block_excl_scan<BS>(sum, tmp, &total);
-#pragma unroll
-  for (int q = 0; q < BPT; ++q) {
-    const int b = tid * BPT + q;
-    if (b < NB) {
-      boff[b] = run;
-      cur[b] = run;
-    }
-    run += c[q];
-  }
+  // exclusive scan of the bucket counts
+  const int total = block_ordered_scan<BS>(
+      NB, [&](int b) { return cur[b]; },
+      [&](int b, int x) {
+        boff[b] = x;
+        cur[b] = x;
+      },
+      tmp);
   if (tid == 0) boff[NB] = total;
   __syncthreads();
   for (int j = tid; j < T; j += BS) {

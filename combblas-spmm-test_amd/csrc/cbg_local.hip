@@ -255,9 +255,22 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
 // accumulate at rank) kernels; a (j, r) holding more than SLAB_CAP nonzeros is
 // cut into row slabs of whole fine ranges.
 // ----------------------------------------------------------------------------
-constexpr int FINE_LOG = 13;            // fine row range = 8192 rows = 256 bitmap words
-constexpr int SLAB_CAP = 12032;         // max nnz of a slab (LDS value array, 94 KiB)
-constexpr int PANEL_LOG_MAX = 18;       // max rows of a panel (LDS bitmap, 32 KiB)
+#ifndef CBG_FINE_LOG
+#define CBG_FINE_LOG 13
+#endif
+#ifndef CBG_SLAB_CAP
+#define CBG_SLAB_CAP 12032
+#endif
+#ifndef CBG_PANEL_LOG_MAX
+#define CBG_PANEL_LOG_MAX 18
+#endif
+#ifndef CBG_SLAB_LARGE_BS
+#define CBG_SLAB_LARGE_BS 1024
+#endif
+constexpr int FINE_LOG = CBG_FINE_LOG;            // fine row range (default 8192 rows = 256 bitmap words)
+constexpr int SLAB_CAP = CBG_SLAB_CAP;            // max nnz of a slab (LDS value array, default 94 KiB)
+constexpr int PANEL_LOG_MAX = CBG_PANEL_LOG_MAX;  // max rows of a panel (LDS bitmap, default 32 KiB)
+static_assert(SLAB_CAP >= (1 << FINE_LOG), "a fine range must fit one slab");
 constexpr int SLAB_WORDS = 1 << (PANEL_LOG_MAX - 5);
 constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= max slabs) per panel
 constexpr int BIG_BS = 512;
@@ -285,7 +298,8 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
                                                       const int32_t* __restrict__ irA, int64_t m, int plog,
                                                       int32_t* __restrict__ cnt, int32_t* __restrict__ cnt_br,
                                                       int4* __restrict__ desc, int32_t* __restrict__ nslab,
-                                                      unsigned* __restrict__ gbm) {
+                                                      unsigned* __restrict__ gbm, int gbm_slots,
+                                                      int* __restrict__ gbm_next, int* __restrict__ gbm_slot) {
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int pwords = 1 << (plog - 5);
@@ -387,23 +401,30 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     __syncthreads();
   }
   }
-  // per fine range popcounts: thread t owns WPT consecutive words inside one
-  // fine range (256 words); G lanes share a fine range and reduce by shuffles
-  const int WPT = max(1, pwords / BS);
-  const int w0 = tid * WPT;
-  int c = 0;
-  unsigned* gdst = gbm ? gbm + (int64_t)br * SLAB_WORDS : nullptr;
-  for (int k = 0; k < WPT; ++k) {
-    const int j = w0 + k;
+  // per fine range popcounts: coalesced words; a wave's 64 words lie in one
+  // fine range (2^(FINE_LOG-5) >= 64 words)
+  static_assert(FINE_LOG - 5 >= 6, "fine range must hold a wave's words");
+  // keep this pair's bitmap for the numeric phase while bitmap slots last
+  unsigned* gdst = nullptr;
+  if (gbm) {
+    if (tid == 0) {
+      int slot = atomicAdd(gbm_next, 1);
+      if (slot >= gbm_slots) slot = -1;
+      gbm_slot[br] = slot;
+      tmp[0] = slot;
+    }
+    __syncthreads();
+    if (tmp[0] >= 0) gdst = gbm + (int64_t)tmp[0] * pwords;
+  }
+  for (int j = tid; j - lane_id() < words; j += BS) {
+    unsigned x = 0;
     if (j < words) {
-      const unsigned x = bm[j];
-      c += __popc(x);
+      x = bm[j];
       if (gdst) gdst[j] = x;
     }
+    const int c = wave_sum(__popc(x));
+    if (lane_id() == 0 && c) atomicAdd(&fine[j >> (FINE_LOG - 5)], c);
   }
-  const int G = min(WAVE, (1 << (FINE_LOG - 5)) / WPT);
-  for (int d = 1; d < G; d <<= 1) c += __shfl_xor(c, d, WAVE);
-  if ((lane_id() & (G - 1)) == 0 && w0 < words && c) atomicAdd(&fine[w0 >> (FINE_LOG - 5)], c);
   __syncthreads();
   if (tid == 0) {
     // greedy slab plan: consecutive fine ranges while the slab holds <= SLAB_CAP
@@ -656,7 +677,7 @@ struct SlabLds {
   static_assert(BYTES <= 160 * 1024, "slab LDS");
 };
 constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
-constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = 1024;
+constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
 template <int SR, int BS>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
@@ -687,7 +708,8 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
                                                  int64_t nA1, const int32_t* __restrict__ irA,
                                                  const double* __restrict__ valA, const int64_t* __restrict__ colptr,
                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val,
-                                                 int64_t m_rows, const unsigned* __restrict__ gbm) {
+                                                 int64_t m_rows, const unsigned* __restrict__ gbm,
+                                                 const int* __restrict__ gbm_slot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
   double* bv = vals + CAP;                                                 // [BS]
@@ -710,9 +732,10 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   const int64_t obase = colptr[col] + d.z;
   const bool full_range = (lo == R0) && (hi == R1);  // the slab is the whole panel
   unsigned long long tmark = wall_clock64();
-  const bool have_bm = gbm != nullptr;  // bitmap kept by the symbolic phase: no marking pass
+  const int slot = gbm ? gbm_slot[e.x] : -1;
+  const bool have_bm = slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
   if (have_bm) {
-    const unsigned* src = gbm + (int64_t)e.x * SLAB_WORDS + ((lo - R0) >> 5);
+    const unsigned* src = gbm + (int64_t)slot * (1 << (plog - 5)) + ((lo - R0) >> 5);
     for (int j = tid; j < words; j += BS) bm[j] = src[j];
   } else {
     for (int j = tid; j < words; j += BS) bm[j] = 0u;
@@ -726,24 +749,8 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   for (int pass = first_pass; pass < 2; ++pass) {
     if (pass == 1) {
       // ranks: exclusive prefix of popcounts over the slab's words
-      constexpr int WPT = (SLAB_WORDS + BS - 1) / BS;
-      int c[WPT];
-      int sum = 0;
-#pragma unroll
-      for (int k = 0; k < WPT; ++k) {
-        const int w = tid * WPT + k;
-        c[k] = (w < words) ? __popc(bm[w]) : 0;
-        sum += c[k];
-      }
-      int total;
-      int run = block_excl_scan<BS>(sum, tmp, &total);
-#pragma unroll
-      for (int k = 0; k < WPT; ++k) {
-        const int w = tid * WPT + k;
-        if (w < words) wpre[w] = (unsigned short)run;
-        run += c[k];
-      }
-      __syncthreads();
+      block_ordered_scan<BS>(
+          words, [&](int w) { return __popc(bm[w]); }, [&](int w, int x) { wpre[w] = (unsigned short)x; }, tmp);
       phase_mark(tmark, 3);
     }
     for (int64_t c0 = p0; c0 < p1; c0 += BS) {
@@ -965,7 +972,8 @@ struct BigPlan {
   DBuf<int2> cmapP;
   DBuf<int4> desc;
   DBuf<int32_t> nslab, cnt_br;
-  DBuf<unsigned> gbm;
+  DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
+  DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
 };
 
 template <int SR, int LOGT, int BS>
@@ -995,7 +1003,7 @@ static void launch_slabs(const int2* list, const int* ncls, const BigPlan& bp, c
     set_lds(k, L);
     hipLaunchKernelGGL(k, dim3((unsigned)ncls[0]), dim3(SLAB_SMALL_BS), L, s, at[0], bp.perm_big, bp.desc.p, bp.R,
                        bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
-                       bp.gbm.p);
+                       bp.gbm.p, bp.gbm_slot.p);
   }
   if (ncls[1] > 0) {
     constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
@@ -1003,7 +1011,7 @@ static void launch_slabs(const int2* list, const int* ncls, const BigPlan& bp, c
     set_lds(k, L);
     hipLaunchKernelGGL(k, dim3((unsigned)ncls[1]), dim3(SLAB_LARGE_BS), L, s, at[1], bp.perm_big, bp.desc.p, bp.R,
                        bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
-                       bp.gbm.p);
+                       bp.gbm.p, bp.gbm_slot.p);
   }
   static_assert(SLAB_HASH_LOG0 == 9 && SLAB_HASH_NCLS == 5, "hash slab classes");
   launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, colptr, C, s);
@@ -1015,7 +1023,7 @@ static void launch_slabs(const int2* list, const int* ncls, const BigPlan& bp, c
 
 static double bitmap_budget_bytes() {
   static const char* e = getenv("CBG_BITMAP_BUDGET_GB");
-  return (e ? atof(e) : 8.0) * 1e9;
+  return (e ? atof(e) : 16.0) * 1e9;
 }
 
 struct Binned {
@@ -1149,13 +1157,23 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     bp.cnt_br.reset(nbr);
     // keep the symbolic bitmaps for the numeric phase when they fit a budget
     // (saves the numeric marking pass); otherwise numeric rebuilds them
-    if ((double)nbr * SLAB_WORDS * 4 <= bitmap_budget_bytes()) bp.gbm.reset((size_t)nbr * SLAB_WORDS);
+    // slots are handed out in launch order by the bitmap-mode pairs
+    const int64_t slot_bytes = (int64_t)4 << (bp.plog - 5);
+    const int64_t nslots = std::min<int64_t>(nbr, (int64_t)(bitmap_budget_bytes() / slot_bytes));
+    DBuf<int> gbm_next;
+    if (nslots > 0) {
+      bp.gbm.reset((size_t)nslots << (bp.plog - 5));
+      bp.gbm_slot.reset(nbr);
+      gbm_next.reset(1);
+      CBG_HIP(hipMemsetAsync(gbm_next.p, 0, sizeof(int), s));
+    }
     const size_t lds = (size_t)(1 << (bp.plog - 5)) * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 +
                        (BIG_BS / WAVE + 4) * 4;
     set_lds(k_sym_panel, lds);
     if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
     hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)nbr), dim3(BIG_BS), lds, s, bp.perm_big, bp.R, B.cp, B.ir,
-                       bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p);
+                       bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p,
+                       (int)nslots, gbm_next.p, bp.gbm_slot.p);
   }
   // column pointers of C
   DBuf<int64_t> colptr(nz + 1);

@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""HBM traffic of one local SpGEMM (the bench's dominant pipeline) from rocprofv3 PMC passes.
+
+  # on the GPU box, one pass per counter group (FETCH_SIZE and WRITE_SIZE do not fit one pass):
+  rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pf -o f -- python3 tools/traffic.py run --scale 18
+  rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pw -o w -- python3 tools/traffic.py run --scale 18
+  # anywhere:
+  python3 tools/traffic.py parse --fetch <f_counter_collection.csv> --write <w_counter_collection.csv> \
+      --meta <run json> --out profiles/r01_traffic_s18.json
+
+`run` issues: digest(A), multiply, digest(A), multiply, digest(C).  The second
+multiply is every dispatch strictly between the 2nd and 3rd k_digest.  The
+digests are the calibration: k_digest reads A's DCSC arrays once, wave per
+column, 4-8 B per lane -- the same access widths as the SpGEMM kernels -- so
+known_bytes / FETCH bytes of digest(A) corrects the gfx950 FETCH_SIZE
+under-count (MI355X_MICROARCH.md, HBM section: FETCH_SIZE reports 1/2 of a wide
+coalesced read; other widths uncalibrated).  WRITE_SIZE is reported as read
+(no store-width calibration is available for 4-8 B/lane stores).
+"""
+import argparse
+import csv
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def tile_bytes(t):
+    return 8 * (t["nzc"] + 1) + 4 * t["nzc"] + 12 * t["nnz"]
+
+
+def run(a):
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from conftest import load_cbg
+    cbg = load_cbg()
+    cbg.lib().cbg_set_device(0)
+    A = cbg.rmat_tile(a.scale, a.ef)
+    B = cbg.rmat_tile(a.scale, a.ef)
+    cbg.synchronize()
+    A.digest()
+    C = cbg.LocalHybridSpGEMM(A, B)
+    cbg.synchronize()
+    C.free()
+    A.digest()
+    C = cbg.LocalHybridSpGEMM(A, B)
+    cbg.synchronize()
+    st = cbg.last_stats()
+    C.digest()
+    meta = {"scale": a.scale, "ef": a.ef,
+            "A": {"nnz": A.nnz, "nzc": A.nzc}, "B": {"nnz": B.nnz, "nzc": B.nzc, "n": B.n},
+            "C": {"nnz": C.nnz, "nzc": C.nzc}, "flops": st["flops"]}
+    print(json.dumps(meta), flush=True)
+
+
+def read_pmc(path, counter):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter:
+                rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    # one value per dispatch (some counters are reported per XCD/instance: sum them)
+    out = {}
+    for d, n, v in rows:
+        if d in out:
+            out[d] = (n, out[d][1] + v)
+        else:
+            out[d] = (n, v)
+    return [(d, n, v) for d, (n, v) in sorted(out.items())]
+
+
+def split(rows):
+    dig = [i for i, (_, n, _) in enumerate(rows) if "k_digest" in n]
+    if len(dig) < 3:
+        raise SystemExit("expected 3 k_digest dispatches, found %d" % len(dig))
+    return rows[dig[0]], rows[dig[1]], rows[dig[2]], rows[dig[1] + 1:dig[2]]
+
+
+def parse(a):
+    meta = None
+    for line in open(a.meta):
+        line = line.strip()
+        if line.startswith("{"):
+            meta = json.loads(line)
+    fr = read_pmc(a.fetch, "FETCH_SIZE")
+    wr = read_pmc(a.write, "WRITE_SIZE")
+    d0, d1, _, mult_f = split(fr)
+    _, _, _, mult_w = split(wr)
+    kb = 1024.0  # rocprofv3 FETCH_SIZE / WRITE_SIZE unit: KiB
+    known_a = tile_bytes(meta["A"])
+    calib = known_a / (0.5 * (d0[2] + d1[2]) * kb)
+    fetch_raw = sum(v for _, _, v in mult_f) * kb
+    write_raw = sum(v for _, _, v in mult_w) * kb
+    per_kernel = {}
+    for _, n, v in mult_f:
+        k = n.split("(")[0]
+        per_kernel.setdefault(k, [0.0, 0.0])[0] += v * kb * calib
+    for _, n, v in mult_w:
+        k = n.split("(")[0]
+        per_kernel.setdefault(k, [0.0, 0.0])[1] += v * kb
+    F, nnzc, nnzb, n = meta["flops"], meta["C"]["nnz"], meta["B"]["nnz"], meta["B"]["n"]
+    alg = 16 * F + 12 * nnzc + 32 * nnzb + 8 * n
+    out = {"scale": meta["scale"], "ef": meta["ef"], "dispatches": len(mult_f),
+           "fetch_calibration": calib, "fetch_bytes_raw": fetch_raw, "fetch_bytes": fetch_raw * calib,
+           "write_bytes": write_raw, "traffic_bytes": fetch_raw * calib + write_raw,
+           "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_raw * calib + write_raw) / alg,
+           "per_kernel_fetch_write": {k: [round(x), round(y)] for k, (x, y) in
+                                      sorted(per_kernel.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))},
+           "meta": meta}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: out[k] for k in ("fetch_calibration", "fetch_bytes", "write_bytes", "traffic_bytes",
+                                          "algorithmic_bytes", "traffic_over_algorithmic")}))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    sub = p.add_subparsers(dest="cmd", required=True)
+    r = sub.add_parser("run")
+    r.add_argument("--scale", type=int, default=18)
+    r.add_argument("--ef", type=int, default=16)
+    q = sub.add_parser("parse")
+    q.add_argument("--fetch", required=True)
+    q.add_argument("--write", required=True)
+    q.add_argument("--meta", required=True)
+    q.add_argument("--out", required=True)
+    a = p.parse_args()
+    run(a) if a.cmd == "run" else parse(a)
+
+
+if __name__ == "__main__":
+    main()
