@@ -452,6 +452,19 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   }
 }
 
+// one numeric work item: everything a slab block needs in one 48-byte load
+struct __attribute__((aligned(16))) SlabRec {
+  int64_t obase;  // first output position in C
+  int64_t p0;     // B column range [p0, p0 + nb)
+  int nb;
+  int r;          // panel
+  int lo, hi;     // row range
+  int nout;       // nnz of the slab
+  int slot;       // kept symbolic bitmap (-1: none)
+  int full;       // the slab is its whole panel
+  int pad;
+};
+
 // slab work lists per launch class.  Classes: 0 bitmap small (nnz <=
 // small_cap), 1 bitmap large, 2+k hash slab with table 2^(SLAB_HASH_LOG0+k).
 constexpr int SLAB_HASH_LOG0 = 9, SLAB_HASH_NCLS = 5;  // tables 512 .. 8192
@@ -497,9 +510,12 @@ __global__ void k_slab_bases(const int* __restrict__ counts, int* __restrict__ c
     }
   }
 }
-// pass 2: (pair, slab) entries into their class segment of one list
+// pass 2: slab records into their class segment of one list
 __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, const int4* __restrict__ desc,
-                            int small_cap, int* __restrict__ cursor, int2* __restrict__ list) {
+                            int small_cap, int* __restrict__ cursor, SlabRec* __restrict__ list,
+                            const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
+                            const int64_t* __restrict__ colptr, const int* __restrict__ gbm_slot, int plog,
+                            int64_t m_rows) {
   __shared__ int lc[SLAB_NCLS], lb[SLAB_NCLS];
   if (threadIdx.x < SLAB_NCLS) lc[threadIdx.x] = 0;
   __syncthreads();
@@ -525,13 +541,29 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
   if (b >= nbig) return;
 #pragma unroll
   for (int c = 0; c < SLAB_NCLS; ++c) o[c] += lb[c];
+  const int col = perm_big[b];
+  const int64_t p0 = cpB[col], nb = cpB[col + 1] - p0, cbase = colptr[col];
   for (int r = 0; r < R; ++r) {
     const int br = b * R + r;
+    const int R0 = r << plog;
+    const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
     for (int s = 0; s < nslab[br]; ++s) {
-      const int c = slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap);
+      const int4 d = desc[(int64_t)br * NFINE_MAX + s];
+      const int c = slab_class(d.w, small_cap);
+      SlabRec rec;
+      rec.obase = cbase + d.z;
+      rec.p0 = p0;
+      rec.nb = (int)nb;
+      rec.r = r;
+      rec.lo = d.x;
+      rec.hi = d.y;
+      rec.nout = d.w & (SLAB_SPARSE - 1);
+      rec.slot = gbm_slot ? gbm_slot[br] : -1;
+      rec.full = (d.x == R0 && d.y == R1);
+      rec.pad = 0;
 #pragma unroll
       for (int q = 0; q < SLAB_NCLS; ++q)
-        if (q == c) list[o[q]++] = make_int2(br, s);
+        if (q == c) list[o[q]++] = rec;
     }
   }
 }
@@ -701,15 +733,12 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
 }
 
 template <int SR, int CAP, int BS>
-__global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
-                                                 const int4* __restrict__ desc, int R, int plog,
-                                                 const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                 const double* __restrict__ valB, const int2* __restrict__ cmapP,
-                                                 int64_t nA1, const int32_t* __restrict__ irA,
-                                                 const double* __restrict__ valA, const int64_t* __restrict__ colptr,
+__global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ list, int plog,
+                                                 const int32_t* __restrict__ irB, const double* __restrict__ valB,
+                                                 const int2* __restrict__ cmapP, int64_t nA1,
+                                                 const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val,
-                                                 int64_t m_rows, const unsigned* __restrict__ gbm,
-                                                 const int* __restrict__ gbm_slot) {
+                                                 const unsigned* __restrict__ gbm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
   double* bv = vals + CAP;                                                 // [BS]
@@ -719,23 +748,18 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   int* tmp = st + BS;                                                      // scan scratch
   unsigned short* wpre = reinterpret_cast<unsigned short*>(tmp + BS / WAVE + 4);  // [SLAB_WORDS]
   const int tid = threadIdx.x;
-  const int2 e = list[blockIdx.x];  // (big column * R + panel, slab)
-  const int4 d = desc[(int64_t)e.x * NFINE_MAX + e.y];
-  const int col = perm_big[e.x / R];
-  const int r = e.x % R;
-  const int R0 = r << plog;
-  const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
-  const int2* cm = cmapP + (int64_t)r * nA1;
-  const int nout = d.w;
-  const int lo = d.x, hi = d.y;
+  const SlabRec rec = list[blockIdx.x];
+  const int R0 = rec.r << plog;
+  const int2* cm = cmapP + (int64_t)rec.r * nA1;
+  const int nout = rec.nout;
+  const int lo = rec.lo, hi = rec.hi;
   const int words = (hi - lo + 31) >> 5;
-  const int64_t obase = colptr[col] + d.z;
-  const bool full_range = (lo == R0) && (hi == R1);  // the slab is the whole panel
+  const int64_t obase = rec.obase;
+  const bool full_range = rec.full;  // the slab is the whole panel
   unsigned long long tmark = wall_clock64();
-  const int slot = gbm ? gbm_slot[e.x] : -1;
-  const bool have_bm = slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
+  const bool have_bm = rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
   if (have_bm) {
-    const unsigned* src = gbm + (int64_t)slot * (1 << (plog - 5)) + ((lo - R0) >> 5);
+    const unsigned* src = gbm + (int64_t)rec.slot * (1 << (plog - 5)) + ((lo - R0) >> 5);
     for (int j = tid; j < words; j += BS) bm[j] = src[j];
   } else {
     for (int j = tid; j < words; j += BS) bm[j] = 0u;
@@ -743,9 +767,8 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
   for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
   __syncthreads();
   phase_mark(tmark, 0);
-  const int64_t p0 = cpB[col], p1 = cpB[col + 1];
-  const bool one_chunk = (p1 - p0) <= BS;
-  const int first_pass = have_bm ? 1 : 0;
+  const int64_t p0 = rec.p0, p1 = rec.p0 + rec.nb;
+  const bool one_chunk = rec.nb <= BS;  const int first_pass = have_bm ? 1 : 0;
   for (int pass = first_pass; pass < 2; ++pass) {
     if (pass == 1) {
       // ranks: exclusive prefix of popcounts over the slab's words
@@ -787,19 +810,22 @@ __global__ __launch_bounds__(BS) void k_num_slab(const int2* __restrict__ list, 
       phase_mark(tmark, 4 + pass);
     }
   }
-  // rows: each word emits its set bits at their ranks; values: coalesced copy
+  // values: coalesced copy; rows: each word scatters its set bits to their
+  // ranks in LDS (reusing the value array), then a coalesced copy
   if (c_dbg & 8) return;
+  for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
+  __syncthreads();
+  int* rows = reinterpret_cast<int*>(vals);
   for (int w = tid; w < words; w += BS) {
     unsigned x = bm[w];
     int pos = wpre[w];
     while (x) {
-      const int bit = __ffs(x) - 1;
+      rows[pos++] = lo + w * 32 + __ffs(x) - 1;
       x &= x - 1;
-      out_ir[obase + pos] = lo + w * 32 + bit;
-      ++pos;
     }
   }
-  for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
+  __syncthreads();
+  for (int j = tid; j < nout; j += BS) out_ir[obase + j] = rows[j];
   if (c_dbg & 16) {
     __syncthreads();
     phase_mark(tmark, 6);
@@ -818,13 +844,11 @@ struct SlabHashLds {
 };
 
 template <int SR, int LOGT, int BS>
-__global__ __launch_bounds__(BS) void k_num_slab_hash(const int2* __restrict__ list, const int32_t* __restrict__ perm_big,
-                                                      const int4* __restrict__ desc, int R, int plog,
-                                                      const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                      const double* __restrict__ valB, const int2* __restrict__ cmapP,
-                                                      int64_t nA1, const int32_t* __restrict__ irA,
-                                                      const double* __restrict__ valA,
-                                                      const int64_t* __restrict__ colptr, int32_t* __restrict__ out_ir,
+__global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int plog,
+                                                      const int32_t* __restrict__ irB, const double* __restrict__ valB,
+                                                      const int2* __restrict__ cmapP, int64_t nA1,
+                                                      const int32_t* __restrict__ irA,
+                                                      const double* __restrict__ valA, int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
   using L = SlabHashLds<LOGT, BS>;
   constexpr int T = L::T, NB = L::NB;
@@ -840,18 +864,15 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const int2* __restrict__ l
   int* cur = boff + NB + 4;
   unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
   const int tid = threadIdx.x;
-  const int2 e = list[blockIdx.x];
-  const int4 d = desc[(int64_t)e.x * NFINE_MAX + e.y];
-  const int col = perm_big[e.x / R];
-  const int r = e.x % R;
-  const int2* cm = cmapP + (int64_t)r * nA1;
+  const SlabRec rec = list[blockIdx.x];
+  const int2* cm = cmapP + (int64_t)rec.r * nA1;
   for (int j = tid; j < T; j += BS) {
     keys[j] = EMPTY_KEY;
     vals[j] = Sem<SR>::identity();
   }
   __syncthreads();
-  const int64_t p1 = cpB[col + 1];
-  for (int64_t c0 = cpB[col]; c0 < p1; c0 += BS) {
+  const int64_t p1 = rec.p0 + rec.nb;
+  for (int64_t c0 = rec.p0; c0 < p1; c0 += BS) {
     const int64_t p = c0 + tid;
     int s = 0, len = 0;
     double bval = 0.0;
@@ -875,7 +896,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const int2* __restrict__ l
     __syncthreads();
   }
   const int bshift = plog > LOGNB ? plog - LOGNB : 0;
-  hash_emit_sorted<T, BS, NB>(keys, vals, d.x, bshift, boff, cur, members, tmp, out_ir, out_val, colptr[col] + d.z);
+  hash_emit_sorted<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val, rec.obase);
 }
 
 // ----------------------------------------------------------------------------
@@ -977,48 +998,45 @@ struct BigPlan {
 };
 
 template <int SR, int LOGT, int BS>
-static void launch_slab_hash(const int2* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                             cbg_tile& C, hipStream_t s) {
   if (n <= 0) return;
   constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
   auto k = k_num_slab_hash<SR, LOGT, BS>;
   set_lds(k, L);
-  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.perm_big, bp.desc.p, bp.R, bp.plog, B.cp, B.ir,
-                     B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val);
+  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.plog, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir,
+                     A.val, C.ir, C.val);
+}
+
+template <int SR, int CAP, int BS>
+static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                               cbg_tile& C, hipStream_t s) {
+  if (n <= 0) return;
+  constexpr int L = SlabLds<CAP, BS>::BYTES;
+  auto k = k_num_slab<SR, CAP, BS>;
+  set_lds(k, L);
+  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.plog, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir,
+                     A.val, C.ir, C.val, bp.gbm.p);
 }
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 template <int SR>
-static void launch_slabs(const int2* list, const int* ncls, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                         const int64_t* colptr, cbg_tile& C, hipStream_t s) {
-  const int2* at[SLAB_NCLS];
+static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp, const cbg_tile& A,
+                         const cbg_tile& B, cbg_tile& C, hipStream_t s) {
+  const SlabRec* at[SLAB_NCLS];
   int64_t o = 0;
   for (int c = 0; c < SLAB_NCLS; ++c) {
     at[c] = list + o;
     o += ncls[c];
   }
-  if (ncls[0] > 0) {
-    constexpr int L = SlabLds<SLAB_SMALL_CAP, SLAB_SMALL_BS>::BYTES;
-    auto k = k_num_slab<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>;
-    set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)ncls[0]), dim3(SLAB_SMALL_BS), L, s, at[0], bp.perm_big, bp.desc.p, bp.R,
-                       bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
-                       bp.gbm.p, bp.gbm_slot.p);
-  }
-  if (ncls[1] > 0) {
-    constexpr int L = SlabLds<SLAB_LARGE_CAP, SLAB_LARGE_BS>::BYTES;
-    auto k = k_num_slab<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>;
-    set_lds(k, L);
-    hipLaunchKernelGGL(k, dim3((unsigned)ncls[1]), dim3(SLAB_LARGE_BS), L, s, at[1], bp.perm_big, bp.desc.p, bp.R,
-                       bp.plog, B.cp, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir, A.val, colptr, C.ir, C.val, A.m,
-                       bp.gbm.p, bp.gbm_slot.p);
-  }
+  launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s);
+  launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s);
   static_assert(SLAB_HASH_LOG0 == 9 && SLAB_HASH_NCLS == 5, "hash slab classes");
-  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, colptr, C, s);
-  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, colptr, C, s);
-  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, colptr, C, s);
-  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, colptr, C, s);
-  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, colptr, C, s);
+  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, C, s);
+  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, C, s);
+  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, C, s);
+  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, C, s);
+  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, C, s);
 }
 
 static double bitmap_budget_bytes() {
@@ -1182,7 +1200,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipMemcpyAsync(&nnzc, colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   // slab lists of big columns
   DBuf<int64_t> sbase;
-  DBuf<int2> slist;
+  DBuf<SlabRec> slist;
   int64_t nslabs = 0;
   if (nbig > 0) {
     sbase.reset(nbr + 1);
@@ -1200,7 +1218,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        bp.desc.p, SLAB_SMALL_CAP, counters.p);
     hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, counters.p, counters.p + SLAB_NCLS);
     hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.desc.p,
-                       SLAB_SMALL_CAP, counters.p + SLAB_NCLS, slist.p);
+                       SLAB_SMALL_CAP, counters.p + SLAB_NCLS, slist.p, bp.perm_big, B.cp, colptr.p, bp.gbm_slot.p,
+                       bp.plog, A.m);
     CBG_HIP(hipMemcpyAsync(ncls, counters.p, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));
   }
@@ -1214,8 +1233,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, colptr.p, C, s);
-    else launch_slabs<0>(slist.p, ncls, bp, A, B, colptr.p, C, s);
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s);
+    else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s);
   }
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);

@@ -177,6 +177,21 @@ def test_summa_single_rank(cbg, algo, exec_mode):
     g.destroy()
 
 
+@pytest.mark.parametrize("algo", ["doublebuff", "synch"])
+@pytest.mark.parametrize("exec_mode", [0, 1])
+def test_summa_rccl_single_rank(cbg, algo, exec_mode):
+    """The RCCL transport end to end on one GPU (1x1 grid: ncclCommInitRank, split, broadcasts)."""
+    g = cbg.CommGrid(0, 1, unique_id=cbg.CommGrid.unique_id(), transport="rccl")
+    A = cbg.SpParMat.rmat(g, 10)
+    B = cbg.SpParMat.rmat(g, 10)
+    f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
+    C = f(A, B, exec_mode=exec_mode)
+    assert_tiles_equal(C.tile.to_host(), load_npz("rmat_s10_ef16_C_local_plus.npz"))
+    assert g.allreduce_max(3.5) == 3.5 and g.allreduce_sum(7) == 7
+    g.barrier()
+    g.destroy()
+
+
 @pytest.mark.parametrize("env", [{"CBG_BITMAP_BUDGET_GB": "0"}, {"CBG_BIG_FLOPS": "64"},
                                  {"CBG_BIG_FLOPS": "64", "CBG_BITMAP_BUDGET_GB": "0"}])
 def test_big_column_path_variants(env):
