@@ -705,7 +705,7 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 template <int CAP, int BS>
 struct SlabLds {
   static constexpr int BYTES =
-      CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4;
+      CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 + 16;
   static_assert(BYTES <= 160 * 1024, "slab LDS");
 };
 constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
@@ -746,7 +746,8 @@ __global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ lis
   int* pref = reinterpret_cast<int*>(bm + SLAB_WORDS);                     // [BS+1]
   int* st = pref + BS + 4;                                                 // [BS]
   int* tmp = st + BS;                                                      // scan scratch
-  unsigned short* wpre = reinterpret_cast<unsigned short*>(tmp + BS / WAVE + 4);  // [SLAB_WORDS]
+  unsigned short* wpre = reinterpret_cast<unsigned short*>(
+      (reinterpret_cast<uintptr_t>(tmp + BS / WAVE + 4) + 15) & ~uintptr_t(15));  // [SLAB_WORDS], 16-B aligned
   const int tid = threadIdx.x;
   const SlabRec rec = list[blockIdx.x];
   const int R0 = rec.r << plog;
@@ -771,9 +772,38 @@ __global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ lis
   const bool one_chunk = rec.nb <= BS;  const int first_pass = have_bm ? 1 : 0;
   for (int pass = first_pass; pass < 2; ++pass) {
     if (pass == 1) {
-      // ranks: exclusive prefix of popcounts over the slab's words
-      block_ordered_scan<BS>(
-          words, [&](int w) { return __popc(bm[w]); }, [&](int w, int x) { wpre[w] = (unsigned short)x; }, tmp);
+      // ranks: exclusive prefix of popcounts over the slab's words; thread t
+      // owns WPT consecutive words, read and written as 16-byte LDS vectors
+      constexpr int WPT = SLAB_WORDS / BS;
+      static_assert(WPT % 8 == 0 && (CAP * 8 + BS * 8) % 16 == 0, "rank scan vectors");
+      const int w0 = tid * WPT;
+      unsigned q[WPT];
+#pragma unroll
+      for (int k = 0; k < WPT; k += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(bm + w0 + k);
+        q[k] = w0 + k < words ? v.x : 0u;
+        q[k + 1] = w0 + k + 1 < words ? v.y : 0u;
+        q[k + 2] = w0 + k + 2 < words ? v.z : 0u;
+        q[k + 3] = w0 + k + 3 < words ? v.w : 0u;
+      }
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < WPT; ++k) sum += __popc(q[k]);
+      int tot;
+      int run = block_excl_scan<BS>(sum, tmp, &tot);
+#pragma unroll
+      for (int k = 0; k < WPT; k += 8) {
+        unsigned pk[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const unsigned a = (unsigned)run;
+          run += __popc(q[k + 2 * h]);
+          pk[h] = a | ((unsigned)run << 16);
+          run += __popc(q[k + 2 * h + 1]);
+        }
+        *reinterpret_cast<uint4*>(wpre + w0 + k) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      }
+      __syncthreads();
       phase_mark(tmark, 3);
     }
     for (int64_t c0 = p0; c0 < p1; c0 += BS) {
