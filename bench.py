@@ -36,6 +36,7 @@ def load_cbg():
 
 
 GRIDS = {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 9: (3, 3), 16: (4, 4)}
+ROUND = "r01"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -53,6 +54,20 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-scale", type=int, default=None, help="scale of the CPU-baseline sample")
     return p.parse_args()
+
+
+def pmc_traffic(scale, ef):
+    """HBM bytes of one local multiply at this scale from the committed PMC passes
+    (profiles/<round>_traffic_s<scale>.json, made by tools/profile_round.sh +
+    tools/traffic.py: FETCH_SIZE calibrated on k_digest, + WRITE_SIZE), or None."""
+    path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (ROUND, scale))
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("scale") != scale or d.get("ef") != ef:
+        return None, None
+    return d["traffic_bytes"], os.path.relpath(path, REPO)
 
 
 def cpu_baseline(scale, ef, seed, threads):
@@ -157,6 +172,7 @@ def main():
     achieved = grid.allreduce_max(achieved) if N > 1 else achieved
 
     if rank == 0:
+        traffic, traffic_src = pmc_traffic(scale, a.ef) if N == 1 else (None, None)
         out = {
             "metric": "nnz(C)/sec for A·A (R-MAT scale %d) at %d GPUs" % (scale, N),
             "value": nnz_c * a.steps / dt,
@@ -176,7 +192,8 @@ def main():
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
                 "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
                          "ms_avg": ms_avg, "bytes_alg": bytes_alg},
         }

@@ -733,132 +733,191 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
 }
 
 template <int SR, int CAP, int BS>
-__global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ list, int plog,
-                                                 const int32_t* __restrict__ irB, const double* __restrict__ valB,
-                                                 const int2* __restrict__ cmapP, int64_t nA1,
-                                                 const int32_t* __restrict__ irA, const double* __restrict__ valA,
-                                                 int32_t* __restrict__ out_ir, double* __restrict__ out_val,
-                                                 const unsigned* __restrict__ gbm) {
+__global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
+                                                 int plog, const int32_t* __restrict__ irB,
+                                                 const double* __restrict__ valB, const int2* __restrict__ cmapP,
+                                                 int64_t nA1, const int32_t* __restrict__ irA,
+                                                 const double* __restrict__ valA, int32_t* __restrict__ out_ir,
+                                                 double* __restrict__ out_val, const unsigned* __restrict__ gbm) {
+  // Persistent blocks (one per CU at this LDS size) pull slabs from a queue.
+  // With one block per CU nothing else hides a slab's dependent global reads,
+  // so the next slab's record, kept bitmap words and B staging (irB/valB,
+  // then the A column map hop) are loaded into registers while the current
+  // slab runs its rank scan, products and output.
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);                          // [CAP]
   double* bv = vals + CAP;                                                 // [BS]
   unsigned* bm = reinterpret_cast<unsigned*>(bv + BS);                     // [SLAB_WORDS]
   int* pref = reinterpret_cast<int*>(bm + SLAB_WORDS);                     // [BS+1]
   int* st = pref + BS + 4;                                                 // [BS]
-  int* tmp = st + BS;                                                      // scan scratch
+  int* tmp = st + BS;                                                      // scan scratch + queue slot
   unsigned short* wpre = reinterpret_cast<unsigned short*>(
       (reinterpret_cast<uintptr_t>(tmp + BS / WAVE + 4) + 15) & ~uintptr_t(15));  // [SLAB_WORDS], 16-B aligned
+  constexpr int WPT = SLAB_WORDS / BS;
+  static_assert(WPT % 8 == 0 && (CAP * 8 + BS * 8) % 16 == 0, "rank scan vectors");
   const int tid = threadIdx.x;
-  const SlabRec rec = list[blockIdx.x];
-  const int R0 = rec.r << plog;
-  const int2* cm = cmapP + (int64_t)rec.r * nA1;
-  const int nout = rec.nout;
-  const int lo = rec.lo, hi = rec.hi;
-  const int words = (hi - lo + 31) >> 5;
-  const int64_t obase = rec.obase;
-  const bool full_range = rec.full;  // the slab is the whole panel
-  unsigned long long tmark = wall_clock64();
-  const bool have_bm = rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
-  if (have_bm) {
-    const unsigned* src = gbm + (int64_t)rec.slot * (1 << (plog - 5)) + ((lo - R0) >> 5);
-    for (int j = tid; j < words; j += BS) bm[j] = src[j];
-  } else {
-    for (int j = tid; j < words; j += BS) bm[j] = 0u;
-  }
-  for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
-  __syncthreads();
-  phase_mark(tmark, 0);
-  const int64_t p0 = rec.p0, p1 = rec.p0 + rec.nb;
-  const bool one_chunk = rec.nb <= BS;  const int first_pass = have_bm ? 1 : 0;
-  for (int pass = first_pass; pass < 2; ++pass) {
-    if (pass == 1) {
-      // ranks: exclusive prefix of popcounts over the slab's words; thread t
-      // owns WPT consecutive words, read and written as 16-byte LDS vectors
-      constexpr int WPT = SLAB_WORDS / BS;
-      static_assert(WPT % 8 == 0 && (CAP * 8 + BS * 8) % 16 == 0, "rank scan vectors");
-      const int w0 = tid * WPT;
-      unsigned q[WPT];
+  const int wslot = 1 << (plog - 5);
+  int i = blockIdx.x;
+  if (i >= n) return;
+  // prefetch registers (bitmap words are coalesced: word k*BS + tid)
+  unsigned pw[WPT];
+  int p_ir = 0;
+  double p_bv = 0.0;
+  int2 p_ce = make_int2(0, 0);
+  auto rec_words = [&](const SlabRec& r) { return (r.hi - r.lo + 31) >> 5; };
+  auto staged = [&](const SlabRec& r) { return r.full && r.nb <= BS; };
+  auto fetch_words = [&](const SlabRec& r) {
+    if (r.slot < 0) return;
+    const unsigned* src = gbm + (int64_t)r.slot * wslot + ((r.lo - (r.r << plog)) >> 5);
+    const int words = rec_words(r);
 #pragma unroll
-      for (int k = 0; k < WPT; k += 4) {
-        const uint4 v = *reinterpret_cast<const uint4*>(bm + w0 + k);
-        q[k] = w0 + k < words ? v.x : 0u;
-        q[k + 1] = w0 + k + 1 < words ? v.y : 0u;
-        q[k + 2] = w0 + k + 2 < words ? v.z : 0u;
-        q[k + 3] = w0 + k + 3 < words ? v.w : 0u;
-      }
-      int sum = 0;
-#pragma unroll
-      for (int k = 0; k < WPT; ++k) sum += __popc(q[k]);
-      int tot;
-      int run = block_excl_scan<BS>(sum, tmp, &tot);
-#pragma unroll
-      for (int k = 0; k < WPT; k += 8) {
-        unsigned pk[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const unsigned a = (unsigned)run;
-          run += __popc(q[k + 2 * h]);
-          pk[h] = a | ((unsigned)run << 16);
-          run += __popc(q[k + 2 * h + 1]);
-        }
-        *reinterpret_cast<uint4*>(wpre + w0 + k) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      }
-      __syncthreads();
-      phase_mark(tmark, 3);
+    for (int k = 0; k < WPT; ++k) {
+      const int j = k * BS + tid;
+      pw[k] = j < words ? src[j] : 0u;
     }
-    for (int64_t c0 = p0; c0 < p1; c0 += BS) {
-      int total;
-      if (pass == first_pass || !one_chunk) {
-        const int64_t p = c0 + tid;
-        int s = 0, len = 0;
-        double bval = 0.0;
-        if (p < p1) {
-          const int2 ce = cm[irB[p]];
-          if (full_range) {
-            s = ce.x;
-            len = ce.y - ce.x;
-          } else if (ce.y > ce.x) {
-            const int a = lower_bound_g(irA, ce.x, ce.y, lo);
-            const int z = lower_bound_g(irA, a, ce.y, hi);
-            s = a;
-            len = z - a;
-          }
-          bval = valB[p];
-        }
-        const int ex = block_excl_scan<BS>(len, tmp, &total);
-        pref[tid] = ex;
-        if (tid == BS - 1) pref[BS] = total;
-        st[tid] = s;
-        bv[tid] = bval;
-        __syncthreads();
-        phase_mark(tmark, 1);
-      } else {
-        total = pref[BS];  // staging of the single chunk is reused by pass 1
-      }
-      if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
-      __syncthreads();
-      phase_mark(tmark, 4 + pass);
+  };
+  auto fetch_stage1 = [&](const SlabRec& r) {
+    if (staged(r) && tid < r.nb) {
+      p_ir = irB[r.p0 + tid];
+      p_bv = valB[r.p0 + tid];
     }
-  }
-  // values: coalesced copy; rows: each word scatters its set bits to their
-  // ranks in LDS (reusing the value array), then a coalesced copy
-  if (c_dbg & 8) return;
-  for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
-  __syncthreads();
-  int* rows = reinterpret_cast<int*>(vals);
-  for (int w = tid; w < words; w += BS) {
-    unsigned x = bm[w];
-    int pos = wpre[w];
-    while (x) {
-      rows[pos++] = lo + w * 32 + __ffs(x) - 1;
-      x &= x - 1;
+  };
+  auto fetch_stage2 = [&](const SlabRec& r) {
+    if (staged(r) && tid < r.nb) p_ce = cmapP[(int64_t)r.r * nA1 + p_ir];
+  };
+  SlabRec rec = list[i];
+  fetch_words(rec);
+  fetch_stage1(rec);
+  fetch_stage2(rec);
+  while (true) {
+    // ---- next work item (its record arrives while this slab fills LDS)
+    if (tid == 0) tmp[BS / WAVE + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    const int2* cm = cmapP + (int64_t)rec.r * nA1;
+    const int nout = rec.nout;
+    const int lo = rec.lo, hi = rec.hi;
+    const int words = rec_words(rec);
+    const int64_t obase = rec.obase;
+    const bool have_bm = rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
+    const bool pre = staged(rec);        // chunk 0 staging came in registers
+    unsigned long long tmark = wall_clock64();
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) {
+      const int j = k * BS + tid;
+      if (j < words) bm[j] = have_bm ? pw[k] : 0u;
     }
-  }
-  __syncthreads();
-  for (int j = tid; j < nout; j += BS) out_ir[obase + j] = rows[j];
-  if (c_dbg & 16) {
+    for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
+    int total = 0;
+    if (pre) {
+      const int len = tid < rec.nb ? p_ce.y - p_ce.x : 0;
+      const int ex = block_excl_scan<BS>(len, tmp, &total);
+      pref[tid] = ex;
+      if (tid == BS - 1) pref[BS] = total;
+      st[tid] = tid < rec.nb ? p_ce.x : 0;
+      bv[tid] = tid < rec.nb ? p_bv : 0.0;
+    }
     __syncthreads();
+    const int inext = tmp[BS / WAVE + 2];
+    const bool has_next = inext < n;
+    SlabRec nrec;
+    if (has_next) nrec = list[inext];
+    phase_mark(tmark, 0);
+    const int64_t p0 = rec.p0, p1 = rec.p0 + rec.nb;
+    const int first_pass = have_bm ? 1 : 0;
+    for (int pass = first_pass; pass < 2; ++pass) {
+      if (pass == 1) {
+        // ranks: exclusive prefix of popcounts over the slab's words; thread t
+        // owns WPT consecutive words, read and written as 16-byte LDS vectors
+        const int w0 = tid * WPT;
+        unsigned q[WPT];
+#pragma unroll
+        for (int k = 0; k < WPT; k += 4) {
+          const uint4 v = *reinterpret_cast<const uint4*>(bm + w0 + k);
+          q[k] = w0 + k < words ? v.x : 0u;
+          q[k + 1] = w0 + k + 1 < words ? v.y : 0u;
+          q[k + 2] = w0 + k + 2 < words ? v.z : 0u;
+          q[k + 3] = w0 + k + 3 < words ? v.w : 0u;
+        }
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) sum += __popc(q[k]);
+        int tot;
+        int run = block_excl_scan<BS>(sum, tmp, &tot);
+#pragma unroll
+        for (int k = 0; k < WPT; k += 8) {
+          unsigned pk[4];
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const unsigned a = (unsigned)run;
+            run += __popc(q[k + 2 * h]);
+            pk[h] = a | ((unsigned)run << 16);
+            run += __popc(q[k + 2 * h + 1]);
+          }
+          *reinterpret_cast<uint4*>(wpre + w0 + k) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
+        __syncthreads();
+        phase_mark(tmark, 3);
+        // next slab: bitmap words and B entries fly while this one multiplies
+        if (has_next) {
+          fetch_words(nrec);
+          fetch_stage1(nrec);
+        }
+      }
+      for (int64_t c0 = p0; c0 < p1; c0 += BS) {
+        if (!(pre && c0 == p0)) {
+          const int64_t p = c0 + tid;
+          int s = 0, len = 0;
+          double bval = 0.0;
+          if (p < p1) {
+            const int2 ce = cm[irB[p]];
+            if (rec.full) {
+              s = ce.x;
+              len = ce.y - ce.x;
+            } else if (ce.y > ce.x) {
+              const int a = lower_bound_g(irA, ce.x, ce.y, lo);
+              const int z = lower_bound_g(irA, a, ce.y, hi);
+              s = a;
+              len = z - a;
+            }
+            bval = valB[p];
+          }
+          const int ex = block_excl_scan<BS>(len, tmp, &total);
+          pref[tid] = ex;
+          if (tid == BS - 1) pref[BS] = total;
+          st[tid] = s;
+          bv[tid] = bval;
+          __syncthreads();
+          phase_mark(tmark, 1);
+        } else {
+          total = pref[BS];
+        }
+        if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+        __syncthreads();
+        phase_mark(tmark, 4 + pass);
+      }
+    }
+    if (has_next) fetch_stage2(nrec);
+    // values: coalesced copy; rows: each word scatters its set bits to their
+    // ranks in LDS (reusing the value array), then a coalesced copy
+    if (!(c_dbg & 8)) {
+      for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
+      __syncthreads();
+      int* rows = reinterpret_cast<int*>(vals);
+      for (int w = tid; w < words; w += BS) {
+        unsigned x = bm[w];
+        int pos = wpre[w];
+        while (x) {
+          rows[pos++] = lo + w * 32 + __ffs(x) - 1;
+          x &= x - 1;
+        }
+      }
+      __syncthreads();
+      for (int j = tid; j < nout; j += BS) out_ir[obase + j] = rows[j];
+    }
+    __syncthreads();  // LDS is refilled by the next slab
     phase_mark(tmark, 6);
+    if (!has_next) break;
+    i = inext;
+    rec = nrec;
   }
 }
 
@@ -1038,6 +1097,16 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
                      A.val, C.ir, C.val);
 }
 
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    CBG_HIP(hipGetDevice(&dev));
+    CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return cus;
+}
+
 template <int SR, int CAP, int BS>
 static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                                cbg_tile& C, hipStream_t s) {
@@ -1045,8 +1114,16 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   constexpr int L = SlabLds<CAP, BS>::BYTES;
   auto k = k_num_slab<SR, CAP, BS>;
   set_lds(k, L);
-  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.plog, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir,
-                     A.val, C.ir, C.val, bp.gbm.p);
+  static int per_cu = 0;
+  if (!per_cu) {
+    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+    if (per_cu < 1) per_cu = 1;
+  }
+  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+  DBuf<int> queue(1);
+  CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
+                     A.n + 1, A.ir, A.val, C.ir, C.val, bp.gbm.p);
 }
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
