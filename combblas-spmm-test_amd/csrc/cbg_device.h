@@ -144,7 +144,26 @@ __device__ __forceinline__ void wave_products(const int* pref, int nseg, int u0,
   int sg = seg_search(pref, nseg, u);
   int nxt = pref[sg + 1];
   auto cur = seg(sg);
-#if CBG_PRODUCTS_U == 4
+#if CBG_PRODUCTS_U >= 8
+  {
+    using X = decltype(load(cur, u));
+    for (; u + (CBG_PRODUCTS_U - 1) * WAVE < u1; u += CBG_PRODUCTS_U * WAVE) {
+      X xs[CBG_PRODUCTS_U];
+#pragma unroll
+      for (int k = 0; k < CBG_PRODUCTS_U; ++k) {
+        const int v = u + k * WAVE;
+        if (v >= nxt) {
+          do nxt = pref[++sg + 1]; while (v >= nxt);
+          cur = seg(sg);
+        }
+        xs[k] = load(cur, v);
+      }
+#pragma unroll
+      for (int k = 0; k < CBG_PRODUCTS_U; ++k) apply(xs[k]);
+    }
+  }
+#endif
+#if CBG_PRODUCTS_U >= 4
   for (; u + 3 * WAVE < u1; u += 4 * WAVE) {
     if (u >= nxt) {
       do nxt = pref[++sg + 1]; while (u >= nxt);

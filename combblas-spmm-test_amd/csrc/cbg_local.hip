@@ -299,7 +299,8 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
                                                       int32_t* __restrict__ cnt, int32_t* __restrict__ cnt_br,
                                                       int4* __restrict__ desc, int32_t* __restrict__ nslab,
                                                       unsigned* __restrict__ gbm, int gbm_slots,
-                                                      int* __restrict__ gbm_next, int* __restrict__ gbm_slot) {
+                                                      int* __restrict__ gbm_next, int* __restrict__ gbm_slot,
+                                                      int gbm_min) {
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int pwords = 1 << (plog - 5);
@@ -318,6 +319,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   const int words = (R1 - R0 + 31) >> 5;
   const int2* cm = cmapP + (int64_t)r * nA1;
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
+  int64_t prod = 0;  // products of the pair
   if (p1 - p0 <= BS) {
     // single chunk: stage once; a pair with few products is counted with an
     // LDS hash sized to it and becomes ONE sparse (hash) slab -- its cost then
@@ -334,6 +336,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = s;
+    prod = total;
     int T = 512;
     while (T < 2 * total) T <<= 1;
     if (total <= SPARSE_SLAB_MAX && T <= pwords) {
@@ -363,6 +366,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
         nslab[br] = cnt_pair ? 1 : 0;
         if (cnt_pair) desc[(int64_t)br * NFINE_MAX] = make_int4(R0, R1, 0, cnt_pair | SLAB_SPARSE);
         cnt_br[br] = cnt_pair;
+        if (gbm_slot) gbm_slot[br] = -1;
         if (cnt_pair) atomicAdd(&cnt[col], cnt_pair);
       }
       return;
@@ -391,6 +395,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
+    prod += total;
     st[tid] = s;
     __syncthreads();
     if (!(c_dbg & 1))
@@ -405,10 +410,12 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   // fine range (2^(FINE_LOG-5) >= 64 words)
   static_assert(FINE_LOG - 5 >= 6, "fine range must hold a wave's words");
   // keep this pair's bitmap for the numeric phase while bitmap slots last
+  // (only for pairs with many products: re-marking a sparse pair in the
+  // numeric phase reads less than storing and reloading its bitmap)
   unsigned* gdst = nullptr;
   if (gbm) {
     if (tid == 0) {
-      int slot = atomicAdd(gbm_next, 1);
+      int slot = prod >= gbm_min ? atomicAdd(gbm_next, 1) : -1;
       if (slot >= gbm_slots) slot = -1;
       gbm_slot[br] = slot;
       tmp[0] = slot;
@@ -1146,6 +1153,13 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, C, s);
 }
 
+// (column, panel) pairs with fewer products re-mark their bitmap in the numeric
+// phase instead of storing it (CBG_GBM_MIN overrides)
+static int gbm_min_products() {
+  static const char* e = getenv("CBG_GBM_MIN");
+  return e ? atoi(e) : 0;
+}
+
 static double bitmap_budget_bytes() {
   static const char* e = getenv("CBG_BITMAP_BUDGET_GB");
   return (e ? atof(e) : 16.0) * 1e9;
@@ -1298,7 +1312,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
     hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)nbr), dim3(BIG_BS), lds, s, bp.perm_big, bp.R, B.cp, B.ir,
                        bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p,
-                       (int)nslots, gbm_next.p, bp.gbm_slot.p);
+                       (int)nslots, gbm_next.p, bp.gbm_slot.p, gbm_min_products());
   }
   // column pointers of C
   DBuf<int64_t> colptr(nz + 1);
