@@ -940,15 +940,21 @@ struct SlabHashLds {
 };
 
 template <int SR, int LOGT, int BS>
-__global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int plog,
-                                                      const int32_t* __restrict__ irB, const double* __restrict__ valB,
-                                                      const int2* __restrict__ cmapP, int64_t nA1,
-                                                      const int32_t* __restrict__ irA,
+__global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
+                                                      int plog, const int32_t* __restrict__ irB,
+                                                      const double* __restrict__ valB, const int2* __restrict__ cmapP,
+                                                      int64_t nA1, const int32_t* __restrict__ irA,
                                                       const double* __restrict__ valA, int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
+  // persistent blocks over a queue of hash slabs; the next slab's record and
+  // B staging (irB/valB, then the A column map hop) are prefetched into
+  // registers while the current slab multiplies and emits (see k_num_slab)
   using L = SlabHashLds<LOGT, BS>;
   constexpr int T = L::T, NB = L::NB;
   constexpr int LOGNB = LOGT - 2;
+  constexpr int NW = BS / WAVE;
+  constexpr int PF = (BIG_BS + BS - 1) / BS;  // prefetched chunks (hash slabs have <= BIG_BS B entries)
+  static_assert(PF <= 2, "prefetch chunks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);
   double* bv = vals + T;
@@ -960,39 +966,85 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   int* cur = boff + NB + 4;
   unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
   const int tid = threadIdx.x;
-  const SlabRec rec = list[blockIdx.x];
-  const int2* cm = cmapP + (int64_t)rec.r * nA1;
-  for (int j = tid; j < T; j += BS) {
-    keys[j] = EMPTY_KEY;
-    vals[j] = Sem<SR>::identity();
-  }
-  __syncthreads();
-  const int64_t p1 = rec.p0 + rec.nb;
-  for (int64_t c0 = rec.p0; c0 < p1; c0 += BS) {
-    const int64_t p = c0 + tid;
-    int s = 0, len = 0;
-    double bval = 0.0;
-    if (p < p1) {
-      const int2 ce = cm[irB[p]];
-      s = ce.x;
-      len = ce.y - ce.x;
-      bval = valB[p];
+  int i = blockIdx.x;
+  if (i >= n) return;
+  int p_ir0 = 0, p_ir1 = 0;
+  double p_bv0 = 0.0, p_bv1 = 0.0;
+  int2 p_ce0 = make_int2(0, 0), p_ce1 = make_int2(0, 0);
+  auto staged = [&](const SlabRec& r) { return r.nb <= PF * BS; };
+  auto fetch1 = [&](const SlabRec& r) {
+    if (!staged(r)) return;
+    if (tid < r.nb) {
+      p_ir0 = irB[r.p0 + tid];
+      p_bv0 = valB[r.p0 + tid];
     }
-    int total;
-    const int ex = block_excl_scan<BS>(len, tmp, &total);
-    pref[tid] = ex;
-    if (tid == BS - 1) pref[BS] = total;
-    st[tid] = s;
-    bv[tid] = bval;
+    if (PF > 1 && BS + tid < r.nb) {
+      p_ir1 = irB[r.p0 + BS + tid];
+      p_bv1 = valB[r.p0 + BS + tid];
+    }
+  };
+  auto fetch2 = [&](const SlabRec& r) {
+    if (!staged(r)) return;
+    const int2* cmr = cmapP + (int64_t)r.r * nA1;
+    if (tid < r.nb) p_ce0 = cmr[p_ir0];
+    if (PF > 1 && BS + tid < r.nb) p_ce1 = cmr[p_ir1];
+  };
+  SlabRec rec = list[i];
+  fetch1(rec);
+  fetch2(rec);
+  while (true) {
+    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    const int2* cm = cmapP + (int64_t)rec.r * nA1;
+    const bool pre = staged(rec);
+    for (int j = tid; j < T; j += BS) {
+      keys[j] = EMPTY_KEY;
+      vals[j] = Sem<SR>::identity();
+    }
     __syncthreads();
-    block_products<BS>(
-        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
-        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
-    __syncthreads();
+    const int inext = tmp[NW + 2];
+    const bool has_next = inext < n;
+    SlabRec nrec;
+    if (has_next) nrec = list[inext];
+    const int64_t p1 = rec.p0 + rec.nb;
+    const int nch = (int)((rec.nb + BS - 1) / BS);
+    for (int c = 0; c < nch; ++c) {
+      const int64_t p = rec.p0 + (int64_t)c * BS + tid;
+      int s = 0, len = 0;
+      double bval = 0.0;
+      if (p < p1) {
+        int2 ce;
+        if (pre) {
+          ce = c == 0 ? p_ce0 : p_ce1;
+          bval = c == 0 ? p_bv0 : p_bv1;
+        } else {
+          ce = cm[irB[p]];
+          bval = valB[p];
+        }
+        s = ce.x;
+        len = ce.y - ce.x;
+      }
+      int total;
+      const int ex = block_excl_scan<BS>(len, tmp, &total);
+      pref[tid] = ex;
+      if (tid == BS - 1) pref[BS] = total;
+      st[tid] = s;
+      bv[tid] = bval;
+      __syncthreads();
+      if (c == nch - 1 && has_next) fetch1(nrec);
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+          [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+          [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
+      __syncthreads();
+    }
+    if (has_next) fetch2(nrec);
+    const int bshift = plog > LOGNB ? plog - LOGNB : 0;
+    hash_emit_sorted<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val, rec.obase);
+    __syncthreads();  // LDS is reset for the next slab
+    if (!has_next) break;
+    i = inext;
+    rec = nrec;
   }
-  const int bshift = plog > LOGNB ? plog - LOGNB : 0;
-  hash_emit_sorted<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val, rec.obase);
 }
 
 // ----------------------------------------------------------------------------
@@ -1093,17 +1145,6 @@ struct BigPlan {
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
 };
 
-template <int SR, int LOGT, int BS>
-static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                             cbg_tile& C, hipStream_t s) {
-  if (n <= 0) return;
-  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS>;
-  set_lds(k, L);
-  hipLaunchKernelGGL(k, dim3((unsigned)n), dim3(BS), L, s, list, bp.plog, B.ir, B.val, bp.cmapP.p, A.n + 1, A.ir,
-                     A.val, C.ir, C.val);
-}
-
 static int device_cus() {
   static int cus = 0;
   if (!cus) {
@@ -1112,6 +1153,25 @@ static int device_cus() {
     CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   return cus;
+}
+
+template <int SR, int LOGT, int BS>
+static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                             cbg_tile& C, hipStream_t s) {
+  if (n <= 0) return;
+  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
+  auto k = k_num_slab_hash<SR, LOGT, BS>;
+  set_lds(k, L);
+  static int per_cu = 0;
+  if (!per_cu) {
+    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+    if (per_cu < 1) per_cu = 1;
+  }
+  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+  DBuf<int> queue(1);
+  CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
+                     A.n + 1, A.ir, A.val, C.ir, C.val);
 }
 
 template <int SR, int CAP, int BS>
