@@ -740,7 +740,7 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
 }
 
 template <int SR, int CAP, int BS>
-__global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
+__global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                  int64_t nA1, const int32_t* __restrict__ irA,
@@ -835,29 +835,33 @@ __global__ __launch_bounds__(BS) void k_num_slab(const SlabRec* __restrict__ lis
         // ranks: exclusive prefix of popcounts over the slab's words; thread t
         // owns WPT consecutive words, read and written as 16-byte LDS vectors
         const int w0 = tid * WPT;
-        unsigned q[WPT];
-#pragma unroll
-        for (int k = 0; k < WPT; k += 4) {
-          const uint4 v = *reinterpret_cast<const uint4*>(bm + w0 + k);
-          q[k] = w0 + k < words ? v.x : 0u;
-          q[k + 1] = w0 + k + 1 < words ? v.y : 0u;
-          q[k + 2] = w0 + k + 2 < words ? v.z : 0u;
-          q[k + 3] = w0 + k + 3 < words ? v.w : 0u;
-        }
+        auto word4 = [&](int k) {  // words w0+k .. w0+k+3, zero past the slab
+          uint4 v = *reinterpret_cast<const uint4*>(bm + w0 + k);
+          if (w0 + k >= words) v.x = 0u;
+          if (w0 + k + 1 >= words) v.y = 0u;
+          if (w0 + k + 2 >= words) v.z = 0u;
+          if (w0 + k + 3 >= words) v.w = 0u;
+          return v;
+        };
         int sum = 0;
 #pragma unroll
-        for (int k = 0; k < WPT; ++k) sum += __popc(q[k]);
+        for (int k = 0; k < WPT; k += 4) {
+          const uint4 v = word4(k);
+          sum += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        }
         int tot;
         int run = block_excl_scan<BS>(sum, tmp, &tot);
 #pragma unroll
         for (int k = 0; k < WPT; k += 8) {
+          const uint4 a = word4(k), b = word4(k + 4);
+          const unsigned q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
           unsigned pk[4];
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
-            const unsigned a = (unsigned)run;
-            run += __popc(q[k + 2 * h]);
-            pk[h] = a | ((unsigned)run << 16);
-            run += __popc(q[k + 2 * h + 1]);
+            const unsigned x = (unsigned)run;
+            run += __popc(q[2 * h]);
+            pk[h] = x | ((unsigned)run << 16);
+            run += __popc(q[2 * h + 1]);
           }
           *reinterpret_cast<uint4*>(wpre + w0 + k) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
         }
