@@ -943,7 +943,9 @@ struct SlabHashLds {
                                (2 * NB + 4) * 4 + (T / 2) * 2;
 };
 
-template <int SR, int LOGT, int BS>
+// CMLEN: cmapP entries are (start, len) -- the whole-column map of the
+// column bins -- instead of the panel maps' (first, end)
+template <int SR, int LOGT, int BS, bool CMLEN>
 __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
@@ -992,6 +994,10 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
     const int2* cmr = cmapP + (int64_t)r.r * nA1;
     if (tid < r.nb) p_ce0 = cmr[p_ir0];
     if (PF > 1 && BS + tid < r.nb) p_ce1 = cmr[p_ir1];
+    if (CMLEN) {
+      p_ce0.y += p_ce0.x;
+      p_ce1.y += p_ce1.x;
+    }
   };
   SlabRec rec = list[i];
   fetch1(rec);
@@ -1022,6 +1028,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
           bval = c == 0 ? p_bv0 : p_bv1;
         } else {
           ce = cm[irB[p]];
+          if (CMLEN) ce.y += ce.x;
           bval = valB[p];
         }
         s = ce.x;
@@ -1074,6 +1081,16 @@ __global__ void k_col_scatter(int64_t n, const int32_t* __restrict__ cnt, const 
 // ----------------------------------------------------------------------------
 void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st);
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    CBG_HIP(hipGetDevice(&dev));
+    CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return cus;
+}
 
 template <class K>
 static void set_lds(K kernel, size_t bytes) {
@@ -1139,6 +1156,49 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
                      A.val, colptr, C.ir, C.val, bshift);
 }
 
+// records of the block hash bins: a column is a hash slab over all rows
+__global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int64_t* __restrict__ cpB,
+                              const int64_t* __restrict__ colptr, SlabRec* __restrict__ rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int col = perm[i];
+  SlabRec r;
+  r.obase = colptr[col];
+  r.p0 = cpB[col];
+  r.nb = (int)(cpB[col + 1] - r.p0);
+  r.r = 0;
+  r.lo = 0;
+  r.hi = 0;
+  r.nout = (int)(colptr[col + 1] - r.obase);
+  r.slot = -1;
+  r.full = 1;
+  r.pad = 0;
+  rec[i] = r;
+}
+
+template <int LOGT, int BS, int SR>
+static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
+                                  const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+  if (n <= 0) return;
+  DBuf<SlabRec> rec(n);
+  hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
+  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
+  auto k = k_num_slab_hash<SR, LOGT, BS, true>;
+  set_lds(k, L);
+  static int per_cu = 0;
+  if (!per_cu) {
+    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+    if (per_cu < 1) per_cu = 1;
+  }
+  int lm = 0;
+  while ((1LL << lm) < A.m) ++lm;  // emit buckets span [0, 2^lm)
+  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+  DBuf<int> queue(1);
+  CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
+                     A.ir, A.val, C.ir, C.val);
+}
+
 struct BigPlan {
   int nbig = 0, R = 1, plog = 0;
   const int32_t* perm_big = nullptr;
@@ -1149,22 +1209,13 @@ struct BigPlan {
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
 };
 
-static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    CBG_HIP(hipGetDevice(&dev));
-    CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return cus;
-}
 
 template <int SR, int LOGT, int BS>
 static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                              cbg_tile& C, hipStream_t s) {
   if (n <= 0) return;
   constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS>;
+  auto k = k_num_slab_hash<SR, LOGT, BS, false>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1266,6 +1317,13 @@ static int pick_panel_log(int64_t m) {
   return l;
 }
 
+// block hash bins through the persistent record-driven hash kernel
+// (CBG_BLOCK_BINS=classic selects the one-block-per-column k_num_block)
+static bool block_bins_persistent() {
+  static const char* e = getenv("CBG_BLOCK_BINS");
+  return !(e && !strcmp(e, "classic"));
+}
+
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
                              const int64_t* colptr, cbg_tile& C, hipStream_t s) {
@@ -1275,10 +1333,17 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_wave<7, SR>(at(2), nb.count[2], B, cmap, A, colptr, C, s);
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
-  launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
-  launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
-  launch_num_block<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s);
-  launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
+  if (block_bins_persistent()) {
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
+  } else {
+    launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
+    launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
+    launch_num_block<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s);
+    launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
+  }
 }
 
 LocalStats& thread_stats() {
