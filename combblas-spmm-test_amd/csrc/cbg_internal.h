@@ -77,6 +77,19 @@ struct DBuf {
   DBuf& operator=(const DBuf&) = delete;
 };
 
+// pool blocks whose release waits until the owner's streams are joined and
+// synchronized (buffers of kernels running on a side stream)
+struct DeferredFree {
+  std::vector<void*> ptrs;
+  template <class T>
+  void take(DBuf<T>& b) {
+    if (b.p) ptrs.push_back(b.detach());
+  }
+  ~DeferredFree() {
+    for (void* q : ptrs) pool().free(q);
+  }
+};
+
 // local SpGEMM (cbg_local.hip)
 struct LocalStats {
   int64_t flops = 0;

@@ -1178,7 +1178,8 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
 
 template <int LOGT, int BS, int SR>
 static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
-                                  const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+                                  const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s,
+                                  DeferredFree& df) {
   if (n <= 0) return;
   DBuf<SlabRec> rec(n);
   hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
@@ -1197,6 +1198,8 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
                      A.ir, A.val, C.ir, C.val);
+  df.take(rec);
+  df.take(queue);
 }
 
 struct BigPlan {
@@ -1212,7 +1215,7 @@ struct BigPlan {
 
 template <int SR, int LOGT, int BS>
 static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                             cbg_tile& C, hipStream_t s) {
+                             cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
   auto k = k_num_slab_hash<SR, LOGT, BS, false>;
@@ -1227,11 +1230,12 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
                      A.n + 1, A.ir, A.val, C.ir, C.val);
+  df.take(queue);
 }
 
 template <int SR, int CAP, int BS>
 static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                               cbg_tile& C, hipStream_t s) {
+                               cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabLds<CAP, BS>::BYTES;
   auto k = k_num_slab<SR, CAP, BS>;
@@ -1246,26 +1250,27 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
                      A.n + 1, A.ir, A.val, C.ir, C.val, bp.gbm.p);
+  df.take(queue);
 }
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 template <int SR>
 static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp, const cbg_tile& A,
-                         const cbg_tile& B, cbg_tile& C, hipStream_t s) {
+                         const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   const SlabRec* at[SLAB_NCLS];
   int64_t o = 0;
   for (int c = 0; c < SLAB_NCLS; ++c) {
     at[c] = list + o;
     o += ncls[c];
   }
-  launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s);
-  launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s);
+  launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s, df);
+  launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s, df);
   static_assert(SLAB_HASH_LOG0 == 9 && SLAB_HASH_NCLS == 5, "hash slab classes");
-  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, C, s);
-  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, C, s);
-  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, C, s);
-  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, C, s);
-  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, C, s);
+  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, C, s, df);
 }
 
 // (column, panel) pairs with fewer products re-mark their bitmap in the numeric
@@ -1326,7 +1331,7 @@ static bool block_bins_persistent() {
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s) {
+                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
   launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, s);
@@ -1334,10 +1339,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
   if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df);
   } else {
     launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
     launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
@@ -1374,6 +1379,23 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (st) *st = LocalStats{};
     return;
   }
+  DeferredFree df;
+  // side stream for the small-column bins (independent of the big columns)
+  static thread_local hipStream_t side = nullptr;
+  static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  if (!side) {
+    CBG_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    CBG_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    CBG_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  }
+  auto fork = [&](hipStream_t main) {
+    CBG_HIP(hipEventRecord(ev_fork, main));
+    CBG_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+  };
+  auto join = [&](hipStream_t main) {
+    CBG_HIP(hipEventRecord(ev_join, side));
+    CBG_HIP(hipStreamWaitEvent(main, ev_join, 0));
+  };
   hipEvent_t ev0, ev1, ev2;
   CBG_HIP(hipEventCreate(&ev0));
   CBG_HIP(hipEventCreate(&ev1));
@@ -1397,15 +1419,17 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
   }
   bin_columns(nz, flops.p, cnt.p, 0, kSymThr, 7, big, sb, s);
+  // small-column symbolic bins on the side stream, big columns on the main one
+  fork(s);
   {
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
-    launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, s);
-    launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, s);
-    launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, s);
-    launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, s);
-    launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, s);
-    launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, s);
+    launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, side);
+    launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, side);
+    launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, side);
+    launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, side);
+    launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, side);
+    launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, side);
   }
   BigPlan bp;
   bp.nbig = sb.count[7];
@@ -1443,6 +1467,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p,
                        (int)nslots, gbm_next.p, bp.gbm_slot.p, gbm_min_products());
   }
+  join(s);
   // column pointers of C
   DBuf<int64_t> colptr(nz + 1);
   exclusive_scan_i32_to_i64(cnt.p, colptr.p, nz, s);
@@ -1480,12 +1505,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // numeric
   Binned nbn;
   bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, s);
-  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, s);
+  // small-column bins on the side stream, big-column slabs on the main one
+  fork(s);
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df);
+  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s);
-    else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s);
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, df);
+    else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, df);
   }
+  join(s);
   // compaction of C's columns
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
