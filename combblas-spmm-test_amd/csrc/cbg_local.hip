@@ -318,6 +318,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), m);
   const int words = (R1 - R0 + 31) >> 5;
   const int2* cm = cmapP + (int64_t)r * nA1;
+  unsigned long long tmark = wall_clock64();
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
   int64_t prod = 0;  // products of the pair
   if (p1 - p0 <= BS) {
@@ -337,6 +338,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = s;
     prod = total;
+    phase_mark(tmark, 8);
     int T = 512;
     while (T < 2 * total) T <<= 1;
     if (total <= SPARSE_SLAB_MAX && T <= pwords) {
@@ -369,6 +371,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
         if (gbm_slot) gbm_slot[br] = -1;
         if (cnt_pair) atomicAdd(&cnt[col], cnt_pair);
       }
+      phase_mark(tmark, 9);
       return;
     }
     for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
@@ -406,6 +409,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     __syncthreads();
   }
   }
+  phase_mark(tmark, 10);
   // per fine range popcounts: coalesced words; a wave's 64 words lie in one
   // fine range (2^(FINE_LOG-5) >= 64 words)
   static_assert(FINE_LOG - 5 >= 6, "fine range must hold a wave's words");
@@ -433,29 +437,49 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
     if (lane_id() == 0 && c) atomicAdd(&fine[j >> (FINE_LOG - 5)], c);
   }
   __syncthreads();
-  if (tid == 0) {
-    // greedy slab plan: consecutive fine ranges while the slab holds <= SLAB_CAP
-    int total = 0, ns = 0;
-    int g_lo = -1, g_hi = 0, g_cnt = 0;
+  phase_mark(tmark, 11);
+  if (tid < WAVE) {
+    // slab plan by wave 0 (nfine <= 64): one slab from the first to the last
+    // non-empty fine range when the pair fits SLAB_CAP, else lane 0 groups
+    // consecutive fine ranges greedily while a slab holds <= SLAB_CAP
+    static_assert(NFINE_MAX <= WAVE, "fine ranges per panel");
+    const int cf = tid < nfine ? fine[tid] : 0;
+    const int total = wave_sum(cf);
+    const unsigned long long nzmask = __ballot(cf != 0);
     int4* d = desc + (int64_t)br * NFINE_MAX;
-    for (int f = 0; f < nfine; ++f) {
-      const int cf = fine[f];
-      if (cf == 0) continue;
-      const int lo = R0 + (f << FINE_LOG);
-      const int hi = min(lo + (1 << FINE_LOG), R1);
-      if (g_cnt && g_cnt + cf > SLAB_CAP) {
-        d[ns++] = make_int4(g_lo, g_hi, total - g_cnt, g_cnt);
-        g_cnt = 0;
+    if (tid == 0) {
+      int ns = 0;
+      if (total > 0 && total <= SLAB_CAP) {
+        const int f0 = __ffsll((long long)nzmask) - 1;
+        const int f1 = 63 - __clzll((long long)nzmask);
+        d[0] = make_int4(R0 + (f0 << FINE_LOG), min(R0 + ((f1 + 1) << FINE_LOG), R1), 0, total);
+        ns = 1;
+      } else if (total > 0) {
+        int run = 0, g_lo = -1, g_hi = 0, g_cnt = 0;
+        for (int f = 0; f < nfine; ++f) {
+          const int c = fine[f];
+          if (c == 0) continue;
+          const int lo = R0 + (f << FINE_LOG);
+          const int hi = min(lo + (1 << FINE_LOG), R1);
+          if (g_cnt && g_cnt + c > SLAB_CAP) {
+            d[ns++] = make_int4(g_lo, g_hi, run - g_cnt, g_cnt);
+            g_cnt = 0;
+          }
+          if (g_cnt == 0) g_lo = lo;
+          g_hi = hi;
+          g_cnt += c;
+          run += c;
+        }
+        if (g_cnt) d[ns++] = make_int4(g_lo, g_hi, run - g_cnt, g_cnt);
       }
-      if (g_cnt == 0) g_lo = lo;
-      g_hi = hi;
-      g_cnt += cf;
-      total += cf;
+      cnt_br[br] = total;
+      nslab[br] = ns;
+      if (total) atomicAdd(&cnt[col], total);
     }
-    if (g_cnt) d[ns++] = make_int4(g_lo, g_hi, total - g_cnt, g_cnt);
-    cnt_br[br] = total;
-    nslab[br] = ns;
-    if (total) atomicAdd(&cnt[col], total);
+  }
+  if (c_dbg & 16) {
+    __syncthreads();
+    phase_mark(tmark, 12);
   }
 }
 
@@ -1538,6 +1562,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       std::fprintf(stderr, "[cbg phases, block-us summed / 256 CUs]");
       for (int k = 0; k < 7; ++k)
         if (k != 2) std::fprintf(stderr, " %s=%.3fms", names[k], ph[k] / 100.0 / 256.0 / 1000.0);
+      const char* snames[5] = {"sym_staging", "sym_hash", "sym_bitmap_products", "sym_counts_store", "sym_plan"};
+      for (int k = 8; k < 13; ++k) std::fprintf(stderr, " %s=%.3fms", snames[k - 8], ph[k] / 100.0 / 256.0 / 1000.0);
       std::fprintf(stderr, "\n");
       std::memset(ph, 0, sizeof(ph));
       CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph)));
