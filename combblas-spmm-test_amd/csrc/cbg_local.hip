@@ -735,8 +735,10 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 // (their phases overlap) while large ones get the full LDS for values.
 template <int CAP, int BS>
 struct SlabLds {
-  static constexpr int BYTES =
-      CAP * 8 + SLAB_WORDS * 4 + SLAB_WORDS * 2 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 + 16;
+  // vals[CAP] f64 | bv[BS] f64 | bm[SLAB_WORDS] | pref[BS+4] | st[BS] | tmp[BS/64+4] | (pad 16) wpre[SLAB_WORDS] u16
+  static constexpr int WPRE_OFF =
+      ((CAP * 8 + BS * 8 + SLAB_WORDS * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4) + 15) & ~15;
+  static constexpr int BYTES = WPRE_OFF + SLAB_WORDS * 2;
   static_assert(BYTES <= 160 * 1024, "slab LDS");
 };
 constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
@@ -782,8 +784,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   int* pref = reinterpret_cast<int*>(bm + SLAB_WORDS);                     // [BS+1]
   int* st = pref + BS + 4;                                                 // [BS]
   int* tmp = st + BS;                                                      // scan scratch + queue slot
-  unsigned short* wpre = reinterpret_cast<unsigned short*>(
-      (reinterpret_cast<uintptr_t>(tmp + BS / WAVE + 4) + 15) & ~uintptr_t(15));  // [SLAB_WORDS], 16-B aligned
+  // [SLAB_WORDS], 16-B aligned; a constant offset from smem keeps the LDS
+  // address space (a uintptr_t round-up would turn its reads into flat loads)
+  unsigned short* wpre = reinterpret_cast<unsigned short*>(smem + SlabLds<CAP, BS>::WPRE_OFF);
   constexpr int WPT = SLAB_WORDS / BS;
   static_assert(WPT % 8 == 0 && (CAP * 8 + BS * 8) % 16 == 0, "rank scan vectors");
   const int tid = threadIdx.x;
