@@ -9,7 +9,7 @@ namespace cbg {
 
 constexpr int WAVE = 64;
 #ifndef CBG_PRODUCTS_U
-#define CBG_PRODUCTS_U 4  // products in flight per lane in wave_products (2 or 4)
+#define CBG_PRODUCTS_U 4  // products in flight per lane in wave_products (2 or 4; 8 measured equal to 4)
 #endif
 constexpr int EMPTY_KEY = 0x7FFFFFFF;  // empty hash slot; sorts after every row id
 
@@ -137,95 +137,82 @@ __device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
 //   seg(sg)        -> SEG           (per segment, e.g. {A offset, B value})
 //   load(SEG, u)   -> X             (global loads of product u)
 //   apply(X)                        (LDS update)
-template <class S, class L, class A>
-__device__ __forceinline__ void wave_products(const int* pref, int nseg, int u0, int u1, S&& seg, L&& load, A&& apply) {
+// pre(X) -> Y runs the apply's reads (e.g. LDS lookups) for all products of
+// an unrolled group before any apply(Y) writes, so their latencies overlap.
+template <class S, class L, class P, class A>
+__device__ __forceinline__ void wave_products3(const int* pref, int nseg, int u0, int u1, S&& seg, L&& load, P&& pre,
+                                               A&& apply) {
   int u = u0 + lane_id();
   if (u >= u1) return;
   int sg = seg_search(pref, nseg, u);
   int nxt = pref[sg + 1];
   auto cur = seg(sg);
-#if CBG_PRODUCTS_U >= 8
-  {
-    using X = decltype(load(cur, u));
-    for (; u + (CBG_PRODUCTS_U - 1) * WAVE < u1; u += CBG_PRODUCTS_U * WAVE) {
-      X xs[CBG_PRODUCTS_U];
-#pragma unroll
-      for (int k = 0; k < CBG_PRODUCTS_U; ++k) {
-        const int v = u + k * WAVE;
-        if (v >= nxt) {
-          do nxt = pref[++sg + 1]; while (v >= nxt);
-          cur = seg(sg);
-        }
-        xs[k] = load(cur, v);
-      }
-#pragma unroll
-      for (int k = 0; k < CBG_PRODUCTS_U; ++k) apply(xs[k]);
+  auto advance = [&](int v) {
+    if (v >= nxt) {
+      do nxt = pref[++sg + 1]; while (v >= nxt);
+      cur = seg(sg);
     }
-  }
-#endif
+  };
 #if CBG_PRODUCTS_U >= 4
   for (; u + 3 * WAVE < u1; u += 4 * WAVE) {
-    if (u >= nxt) {
-      do nxt = pref[++sg + 1]; while (u >= nxt);
-      cur = seg(sg);
-    }
+    advance(u);
     auto x0 = load(cur, u);
-    int v = u + WAVE;
-    if (v >= nxt) {
-      do nxt = pref[++sg + 1]; while (v >= nxt);
-      cur = seg(sg);
-    }
-    auto x1 = load(cur, v);
-    v += WAVE;
-    if (v >= nxt) {
-      do nxt = pref[++sg + 1]; while (v >= nxt);
-      cur = seg(sg);
-    }
-    auto x2 = load(cur, v);
-    v += WAVE;
-    if (v >= nxt) {
-      do nxt = pref[++sg + 1]; while (v >= nxt);
-      cur = seg(sg);
-    }
-    auto x3 = load(cur, v);
-    apply(x0);
-    apply(x1);
-    apply(x2);
-    apply(x3);
+    advance(u + WAVE);
+    auto x1 = load(cur, u + WAVE);
+    advance(u + 2 * WAVE);
+    auto x2 = load(cur, u + 2 * WAVE);
+    advance(u + 3 * WAVE);
+    auto x3 = load(cur, u + 3 * WAVE);
+    auto y0 = pre(x0);
+    auto y1 = pre(x1);
+    auto y2 = pre(x2);
+    auto y3 = pre(x3);
+    apply(y0);
+    apply(y1);
+    apply(y2);
+    apply(y3);
   }
 #endif
   for (; u + WAVE < u1; u += 2 * WAVE) {
-    if (u >= nxt) {
-      do nxt = pref[++sg + 1]; while (u >= nxt);
-      cur = seg(sg);
-    }
+    advance(u);
     auto x0 = load(cur, u);
-    const int v = u + WAVE;
-    if (v >= nxt) {
-      do nxt = pref[++sg + 1]; while (v >= nxt);
-      cur = seg(sg);
-    }
-    auto x1 = load(cur, v);
-    apply(x0);
-    apply(x1);
+    advance(u + WAVE);
+    auto x1 = load(cur, u + WAVE);
+    auto y0 = pre(x0);
+    auto y1 = pre(x1);
+    apply(y0);
+    apply(y1);
   }
   if (u < u1) {
-    if (u >= nxt) {
-      do nxt = pref[++sg + 1]; while (u >= nxt);
-      cur = seg(sg);
-    }
-    apply(load(cur, u));
+    advance(u);
+    apply(pre(load(cur, u)));
   }
 }
 
-// block-wide version: wave w takes the contiguous range [w*per, (w+1)*per)
-template <int BS, class S, class L, class A>
-__device__ __forceinline__ void block_products(const int* pref, int total, S&& seg, L&& load, A&& apply) {
+struct PreIdentity {
+  template <class X>
+  __device__ __forceinline__ X operator()(const X& x) const {
+    return x;
+  }
+};
+
+template <class S, class L, class A>
+__device__ __forceinline__ void wave_products(const int* pref, int nseg, int u0, int u1, S&& seg, L&& load, A&& apply) {
+  wave_products3(pref, nseg, u0, u1, seg, load, PreIdentity(), apply);
+}
+
+// block-wide versions: wave w takes the contiguous range [w*per, (w+1)*per)
+template <int BS, class S, class L, class P, class A>
+__device__ __forceinline__ void block_products3(const int* pref, int total, S&& seg, L&& load, P&& pre, A&& apply) {
   constexpr int NW = BS / WAVE;
   const int w = threadIdx.x / WAVE;
   const int per = (total + NW - 1) / NW;
   const int u0 = min(w * per, total), u1 = min(u0 + per, total);
-  wave_products(pref, BS, u0, u1, seg, load, apply);
+  wave_products3(pref, BS, u0, u1, seg, load, pre, apply);
+}
+template <int BS, class S, class L, class A>
+__device__ __forceinline__ void block_products(const int* pref, int total, S&& seg, L&& load, A&& apply) {
+  block_products3<BS>(pref, total, seg, load, PreIdentity(), apply);
 }
 
 // per-segment register cache: A offset (st[sg] - pref[sg]) and B value

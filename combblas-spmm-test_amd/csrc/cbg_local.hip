@@ -754,14 +754,15 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
         [&](const SegI& g, int u) { return irA[g.off + u] - lo; },
         [&](int r) { atomicOr(&bm[r >> 5], 1u << (r & 31)); });
   } else {
-    block_products<BS>(
+    // ranks of a group of products are looked up before any accumulates
+    block_products3<BS>(
         pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
         [&](const SegV& g, int u) { return RowVal{irA[g.off + u] - lo, Sem<SR>::mul(valA[g.off + u], g.b)}; },
         [&](const RowVal& x) {
           const int w = x.row >> 5;
-          const int pos = wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u));
-          Sem<SR>::lds_acc(&vals[pos], x.v);
-        });
+          return RowVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.v};
+        },
+        [&](const RowVal& x) { Sem<SR>::lds_acc(&vals[x.row], x.v); });
   }
 }
 
