@@ -1525,6 +1525,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        bp.plog, A.m);
     CBG_HIP(hipMemcpyAsync(ncls, counters.p, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));
+    static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
+    if (dbg & 16)
+      std::fprintf(stderr, "[cbg slabs] bitmap small %d large %d | hash T512 %d T1024 %d T2048 %d T4096 %d T8192 %d\n",
+                   ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5], ncls[6]);
   }
   // output arrays
   C.nnz = nnzc;

@@ -41,7 +41,7 @@ def test_host_transport_cpu(grid, case, transport):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4)])
+@pytest.mark.parametrize("grid", [(1, 2), (2, 1), (2, 2), (2, 4), (4, 2)])
 @pytest.mark.parametrize("case", ["rmat", "largeseq"])
 def test_summa_multiprocess_gpu(grid, case):
     rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), case], timeout=600)
