@@ -52,14 +52,29 @@ __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int3
   if (i < nzc) cmap[jc[i]] = make_int2((int)cp[i], (int)(cp[i + 1] - cp[i]));
 }
 
+// flops of every B column: FLOP_G lanes per column (B columns are short on
+// average; a whole wave per column would leave most lanes idle)
+constexpr int FLOP_G = 16;
 __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
                         const int2* __restrict__ cmap, int64_t* __restrict__ flops) {
-  int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
-  if (w >= nzcB) return;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t w = t / FLOP_G;
+  const int g = (int)(t % FLOP_G);
   long long s = 0;
-  for (int64_t p = cpB[w] + lane_id(); p < cpB[w + 1]; p += WAVE) s += cmap[irB[p]].y;
-  s = wave_sum64(s);
-  if (lane_id() == 0) flops[w] = s;
+  if (w < nzcB)
+    for (int64_t p = cpB[w] + g; p < cpB[w + 1]; p += FLOP_G) s += cmap[irB[p]].y;
+#pragma unroll
+  for (int d = FLOP_G / 2; d > 0; d >>= 1) s += __shfl_xor(s, d, FLOP_G);
+  if (w < nzcB && g == 0) flops[w] = s;
+}
+
+// panel column map when A has a single row panel: {start, end} from cmap
+__global__ void k_colmap_panel1(int64_t nA1, const int2* __restrict__ cmap, int2* __restrict__ cmapP) {
+  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (k < nA1) {
+    const int2 e = cmap[k];
+    cmapP[k] = make_int2(e.x, e.x + e.y);
+  }
 }
 
 constexpr int MAXBINS = 12;
@@ -280,10 +295,11 @@ constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in
 // cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r
 __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
                                 const int32_t* __restrict__ irA, int plog, int64_t nA1, int2* __restrict__ cmapP) {
-  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t i = t / FLOP_G;  // FLOP_G lanes per A column
   if (i >= nzcA) return;
   const int64_t k = jcA[i], a = cpA[i], e = cpA[i + 1];
-  for (int64_t q = a + lane_id(); q < e; q += WAVE) {
+  for (int64_t q = a + t % FLOP_G; q < e; q += FLOP_G) {
     const int pnl = irA[q] >> plog;
     if (q == a || (irA[q - 1] >> plog) != pnl) cmapP[pnl * nA1 + k].x = (int)q;
     if (q == e - 1 || (irA[q + 1] >> plog) != pnl) cmapP[pnl * nA1 + k].y = (int)(q + 1);
@@ -1436,7 +1452,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
-  hipLaunchKernelGGL(k_flops, dim3(nblk(nz * WAVE, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p);
+  hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p);
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
@@ -1469,9 +1485,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (nbig > 0) {
     // panel column maps of A
     bp.cmapP.reset((size_t)bp.R * (A.n + 1));
-    CBG_HIP(hipMemsetAsync(bp.cmapP.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
-    hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * WAVE, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
-                       bp.plog, A.n + 1, bp.cmapP.p);
+    if (bp.R == 1) {
+      hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, bp.cmapP.p);
+    } else {
+      CBG_HIP(hipMemsetAsync(bp.cmapP.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
+      hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * FLOP_G, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
+                         bp.plog, A.n + 1, bp.cmapP.p);
+    }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
     bp.nslab.reset(nbr);
     bp.cnt_br.reset(nbr);
