@@ -68,7 +68,12 @@ EXPORTS = [
     "cbg_tile_split_rows", "cbg_tile_digest", "cbg_rmat_tile", "cbg_local_spgemm", "cbg_local_symbolic", "cbg_merge",
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
+    "cbg_tile_equal", "cbg_summa_spgemm_phased",
 ]
+
+# int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg_tile* C_phase)
+PHASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p)
+EPSILON = 0.01  # SpDefs.h:64, the tolerance of ErrorTolerantEqual
 
 _lib = None
 
@@ -113,6 +118,8 @@ def lib():
         "cbg_grid_allreduce_max": ([vp, ctypes.POINTER(ctypes.c_double)], i32),
         "cbg_grid_allreduce_sum_i64": ([vp, ctypes.POINTER(i64)], i32),
         "cbg_summa_spgemm": ([vp, T, T, i64, i64, i32, i32, i32, T], i32),
+        "cbg_tile_equal": ([T, T, ctypes.c_double, ctypes.POINTER(i32)], i32),
+        "cbg_summa_spgemm_phased": ([vp, T, T, i64, i64, i32, i32, i32, i32, PHASE_FN, vp, T], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -177,6 +184,17 @@ class Tile:
                                      ctypes.byref(vs)))
         return dict(nnz=int(self.c.nnz), nzc=int(self.c.nzc), hs="%016x" % hs.value, hv="%016x" % hv.value,
                     vsum=vs.value)
+
+    def equal(self, other, epsilon=EPSILON):
+        """SpDCCols::operator== (SpDCCols.h:74-81): exact structure, ErrorTolerantEqual values."""
+        eq = ctypes.c_int()
+        _check(lib().cbg_tile_equal(ctypes.byref(self.c), ctypes.byref(other.c), epsilon, ctypes.byref(eq)))
+        return bool(eq.value)
+
+    def __eq__(self, other):
+        return isinstance(other, Tile) and self.equal(other)
+
+    __hash__ = object.__hash__
 
     def split_cols(self, cut):
         """SpDCCols::Split (SpDCCols.cpp:905-930)"""
@@ -532,6 +550,17 @@ class SpParMat:
         """global nnz (SpParMat::getnnz Allreduce, SpParMat.cpp:772-778)"""
         return self.grid.allreduce_sum(self.tile.nnz) if self.grid is not None else self.tile.nnz
 
+    def __eq__(self, other):
+        """SpParMat::operator== (SpParMat.cpp:2878-2884): local tile equality, AND over the grid."""
+        if not isinstance(other, SpParMat):
+            return False
+        local = 1 if self.tile.equal(other.tile) else 0
+        if self.grid is None:
+            return bool(local)
+        return self.grid.allreduce_sum(1 - local) == 0
+
+    __hash__ = object.__hash__
+
     @staticmethod
     def rmat(grid, scale, edgefactor=16, seed=0xDECAFBAD):
         nv = 1 << scale
@@ -578,6 +607,40 @@ def Mult_AnXBn_DoubleBuff(A, B, sr=PlusTimesSRing, exec_mode=EXEC_PANEL):
 def Mult_AnXBn_Synch(A, B, sr=PlusTimesSRing, exec_mode=EXEC_PANEL):
     """ParFriends.h:1004-1108 (collective over A.grid)."""
     return _summa(A, B, sr, SYNCH, exec_mode)
+
+
+def MemEfficientSpGEMM(A, B, phases, sr=PlusTimesSRing, algo=DOUBLEBUFF, exec_mode=EXEC_PANEL, on_phase=None,
+                       hardThreshold=0.0, selectNum=0, recoverNum=0, recoverPct=0.0):
+    """ParFriends.h:449-730 with `phases` column pieces of B; the MCL pruning
+    arguments must stay at their no-pruning values (pruning is not on this path).
+
+    on_phase=None: C is the column concatenation of the phase products
+    (ColConcatenate).  on_phase=fn: fn(phase, col_offset, Tile) is called with
+    each phase's device tile (valid during the call only) and None is returned."""
+    if hardThreshold > 0 or selectNum > 0 or recoverNum > 0 or recoverPct > 0:
+        raise CbgError(INVALIDPARAMS, "MemEfficientSpGEMM pruning (MCL) is not supported on this path")
+    errors = []  # (A is B is allowed: the reference copies B, ParFriends.h:547-549)
+
+    def _cb(user, phase, off, ptile):
+        try:
+            view = Tile(CTile.from_buffer_copy(CTile.from_address(ptile)))
+            try:
+                on_phase(phase, int(off), view)
+            finally:
+                view.c = CTile()  # borrowed: libcbg frees the phase tile after the call
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported after the collective finishes
+            errors.append(e)
+            return 1
+
+    fn = PHASE_FN(_cb) if on_phase is not None else PHASE_FN()
+    C = Tile() if on_phase is None else None
+    rc = lib().cbg_summa_spgemm_phased(A.grid.h, ctypes.byref(A.tile.c), ctypes.byref(B.tile.c), A.gn, B.gm, _sr(sr),
+                                       algo, exec_mode, phases, fn, None, ctypes.byref(C.c) if C else None)
+    if errors:
+        raise errors[0]
+    _check(rc)
+    return SpParMat(C, A.grid, A.gm, B.gn) if C is not None else None
 
 
 def PSpGEMM(A, B, sr=PlusTimesSRing):

@@ -10,6 +10,7 @@ namespace cbg {
 void rmat_tile(int scale, int ef, uint64_t userseed, int pr, int pc, int prow, int pcol, cbg_tile& out, hipStream_t s);
 void tile_digest(const cbg_tile& t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum,
                  hipStream_t s);
+bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s);
 int grid_shape(int nranks, int& rows, int& cols);
 cbg_grid* grid_create_rccl(int rank, int nranks, int rows, int cols, const void* uid);
 cbg_grid* grid_create_host(int rank, int nranks, int rows, int cols, const cbg_host_comm* hc);
@@ -19,6 +20,8 @@ void allreduce_sum_i64(cbg_grid* g, int64_t* v);
 void barrier(cbg_grid* g);
 int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr, int algo,
                  int exec, cbg_tile& C);
+int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
+                        int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C);
 }  // namespace cbg
 
 namespace {
@@ -171,6 +174,16 @@ int cbg_tile_digest(const cbg_tile* t, int64_t roff, int64_t coff, uint64_t* hs,
   });
 }
 
+int cbg_tile_equal(const cbg_tile* a, const cbg_tile* b, double epsilon, int* equal) {
+  if (int rc = check_tile(a, true, "a")) return rc;
+  if (int rc = check_tile(b, true, "b")) return rc;
+  if (!equal || !(epsilon >= 0)) return fail(CBG_ERR_INVALIDPARAMS, "bad equality parameters");
+  return guard([&] {
+    *equal = cbg::tile_equal(*a, *b, epsilon, default_stream()) ? 1 : 0;
+    return CBG_OK;
+  });
+}
+
 int cbg_rmat_tile(int scale, int ef, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile* out) {
   if (scale < 1 || scale > 30 || ef < 1 || pr < 1 || pc < 1 || prow < 0 || prow >= pr || pcol < 0 || pcol >= pc || !out)
     return fail(CBG_ERR_INVALIDPARAMS, "bad R-MAT parameters");
@@ -302,6 +315,28 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t 
                             : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
                             : rc == CBG_ERR_NOTSQUARE   ? "staged SUMMA needs a square grid"
                                                         : "summa failed");
+    return CBG_OK;
+  });
+}
+
+int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow,
+                            int sr, int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+  if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  if (int rc = check_tile(A, true, "A")) return rc;
+  if (int rc = check_tile(B, true, "B")) return rc;  // A and B may alias: B is copied (ParFriends.h:547-549)
+  if ((!C && !fn) || (sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) || (algo != CBG_DOUBLEBUFF && algo != CBG_SYNCH) ||
+      (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
+    return fail(CBG_ERR_INVALIDPARAMS, "bad phased summa parameters");
+  return guard([&]() -> int {
+    cbg::thread_stats() = cbg::LocalStats{};
+    CBG_HIP(hipDeviceSynchronize());
+    int rc = cbg::summa_spgemm_phased(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, phases, fn, user, C);
+    if (rc) return fail(rc, rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"
+                            : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
+                            : rc == CBG_ERR_NOTSQUARE   ? "staged SUMMA needs a square grid"
+                            : rc == CBG_ERR_INVALIDPARAMS
+                                ? "phases: a B tile has fewer columns than phases, or a phase callback failed"
+                                : "phased summa failed");
     return CBG_OK;
   });
 }

@@ -120,5 +120,6 @@ void tile_concat_cols(const std::vector<cbg_tile>& parts, const std::vector<int6
                       int64_t n, cbg_tile& out, hipStream_t s);
 void tile_concat_rows(const std::vector<cbg_tile>& parts, const std::vector<int64_t>& row_off, int64_t m,
                       int64_t n, cbg_tile& out, hipStream_t s);
+bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s);
 
 }  // namespace cbg

@@ -334,6 +334,78 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
   return CBG_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// MemEfficientSpGEMM (ParFriends.h:449-730) minus its Markov-clustering pruning:
+// B's local tile is cut into `phases` column pieces like SpDCCols::ColSplit
+// (SpDCCols.cpp:936-970), each piece goes through summa_spgemm, and the phase
+// results are streamed to `fn` or column-concatenated (ColConcatenate,
+// ParFriends.h:724-725).  Column pieces keep every C column's products inside
+// one phase, so the result is identical to the unphased product.
+// ---------------------------------------------------------------------------
+int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
+                        int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+  if (phases < 1 || phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
+  int64_t small = B.n < phases ? 1 : 0;              // ColSplit: "Matrix is too small to be splitted"
+  allreduce_sum_i64(g, &small);
+  if (small) return CBG_ERR_INVALIDPARAMS;
+  hipStream_t cs = g->compute;
+  // column pieces of B: [p * (n / phases), (p + 1) * (n / phases)), the last takes the rest
+  std::vector<cbg_tile> pieces(phases);
+  std::vector<int64_t> off(phases);
+  const int64_t w = B.n / phases;
+  // the reference copies B first, so A and B may alias here (ParFriends.h:547-549)
+  const bool alias = (&A == &B) || (A.ir == B.ir && A.nnz > 0);
+  const bool copied = phases > 1 || alias;
+  if (!copied) {
+    pieces[0] = B;
+  } else if (phases == 1) {
+    cbg_tile right{};
+    tile_split_cols(B, B.n, pieces[0], right, cs);
+    tile_free_device(right);
+  } else {
+    cbg_tile rest = B;
+    for (int p = 0; p < phases - 1; ++p) {
+      cbg_tile left{}, right{};
+      tile_split_cols(rest, w, left, right, cs);
+      if (p > 0) tile_free_device(rest);
+      pieces[p] = left;
+      rest = right;
+    }
+    pieces[phases - 1] = rest;
+  }
+  for (int p = 0; p < phases; ++p) off[p] = (int64_t)p * w;
+  std::vector<cbg_tile> parts;
+  int cb_rc = 0;
+  for (int p = 0; p < phases; ++p) {
+    cbg_tile Cp{};
+    const int rc = summa_spgemm(g, A, pieces[p], A_gncol, B_gnrow, sr, algo, exec, Cp);
+    if (copied) tile_free_device(pieces[p]);
+    if (rc) {
+      for (int q = p + 1; q < phases; ++q)
+        if (copied) tile_free_device(pieces[q]);
+      for (auto& t : parts) tile_free_device(t);
+      return rc;
+    }
+    if (fn) {
+      CBG_HIP(hipStreamSynchronize(cs));
+      const int r = fn(user, p, off[p], &Cp);
+      if (r && !cb_rc) cb_rc = r;
+      tile_free_device(Cp);
+    } else {
+      parts.push_back(Cp);
+    }
+  }
+  if (fn) return cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK;
+  if (parts.size() == 1) {
+    *C = parts[0];
+  } else {
+    tile_concat_cols(parts, off, A.m, B.n, *C, cs);
+    for (auto& t : parts) tile_free_device(t);
+  }
+  return CBG_OK;
+}
+
 }  // namespace cbg
 
 extern "C" int cbg_get_unique_id(void* id) {

@@ -465,4 +465,47 @@ void tile_digest(const cbg_tile& t, int64_t roff, int64_t coff, uint64_t* hs, ui
   *hv = h[1];
 }
 
+// ---------------------------------------------------------------------------
+// SpDCCols::operator== (SpDCCols.h:74-81) + Dcsc::operator== (dcsc.cpp:472-510):
+// structure exact (cp, jc, ir), values ErrorTolerantEqual (Compare.h:47-65):
+// a == b, or |a-b| < eps, or |a-b| / max(|a|,|b|) < eps (eps = SpDefs.h:64 EPSILON)
+// ---------------------------------------------------------------------------
+__global__ void k_tile_diff(int64_t nzc, int64_t nnz, const int64_t* __restrict__ cpa,
+                            const int64_t* __restrict__ cpb, const int32_t* __restrict__ jca,
+                            const int32_t* __restrict__ jcb, const int32_t* __restrict__ ira,
+                            const int32_t* __restrict__ irb, const double* __restrict__ va,
+                            const double* __restrict__ vb, double eps, unsigned long long* __restrict__ bad) {
+  unsigned long long mine = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz || i <= nzc; i += stride) {
+    if (i <= nzc && cpa[i] != cpb[i]) ++mine;
+    if (i < nzc && jca[i] != jcb[i]) ++mine;
+    if (i < nnz) {
+      if (ira[i] != irb[i]) ++mine;
+      const double a = va[i], b = vb[i];
+      if (!(a == b)) {
+        const double d = fabs(a - b);
+        if (!(d < eps || d / fmax(fabs(a), fabs(b)) < eps)) ++mine;
+      }
+    }
+  }
+  mine = wave_sum64((long long)mine);
+  if (lane_id() == 0 && mine) atomicAdd(bad, mine);
+}
+
+bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s) {
+  if (a.nnz == 0 && b.nnz == 0) return true;
+  if (a.nnz != b.nnz || a.m != b.m || a.n != b.n || a.nzc != b.nzc) return false;
+  DBuf<unsigned long long> bad(1);
+  CBG_HIP(hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), s));
+  const int64_t work = std::max(a.nnz, a.nzc + 1);
+  const unsigned blocks = (unsigned)std::min<int64_t>((work + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_tile_diff, dim3(blocks), dim3(256), 0, s, a.nzc, a.nnz, a.cp, b.cp, a.jc, b.jc, a.ir, b.ir,
+                     a.val, b.val, eps, bad.p);
+  unsigned long long h = 0;
+  CBG_HIP(hipMemcpyAsync(&h, bad.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  return h == 0;
+}
+
 }  // namespace cbg

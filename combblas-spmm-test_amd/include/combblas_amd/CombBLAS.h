@@ -10,6 +10,8 @@
 //   Mult_AnXBn_DoubleBuff      ParFriends.h:798   Mult_AnXBn_DoubleBuff
 //   Mult_AnXBn_Synch           ParFriends.h:1004  Mult_AnXBn_Synch
 //   PSpGEMM                    SpParMat.h:454     PSpGEMM
+//   MemEfficientSpGEMM         ParFriends.h:449   MemEfficientSpGEMM (phases; no MCL pruning)
+//   SpDCCols/SpParMat ==       SpDCCols.h:74, SpParMat.cpp:2878  operator== (ErrorTolerantEqual)
 //
 // Same template parameters and call shapes, so MultTiming/MultTest-style
 // drivers (tools/multtiming.cpp) compile against it.  Misuse that the
@@ -109,6 +111,12 @@ class SpDCCols {
   int64_t getnnz() const { return t_.nnz; }
   int64_t getnzc() const { return t_.nzc; }
   bool isZero() const { return t_.nnz == 0; }
+  // SpDCCols::operator== (SpDCCols.h:74-81): exact structure, values within EPSILON (SpDefs.h:64)
+  bool operator==(const SpDCCols& rhs) const {
+    int eq = 0;
+    cbg_abort_on(cbg_tile_equal(&t_, &rhs.t_, 0.01, &eq), "SpDCCols::operator==");
+    return eq != 0;
+  }
   std::vector<IT> GetEssentials() const { return {(IT)t_.nnz, (IT)t_.m, (IT)t_.n, (IT)t_.nzc}; }
   const cbg_tile* tile() const { return &t_; }
   cbg_tile* tile() { return &t_; }
@@ -227,6 +235,12 @@ class SpParMat {
   }
   DER& seq() const { return *spSeq; }
   std::shared_ptr<CommGrid> getcommgrid() const { return commGrid; }
+  // SpParMat::operator== (SpParMat.cpp:2878-2884): local equality, AND over the grid
+  bool operator==(const SpParMat& rhs) const {
+    int64_t bad = (*spSeq == *rhs.spSeq) ? 0 : 1;
+    cbg_abort_on(cbg_grid_allreduce_sum_i64(commGrid->handle(), &bad), "SpParMat::operator==");
+    return bad == 0;
+  }
 
   DER* spSeq = nullptr;
   std::shared_ptr<CommGrid> commGrid;
@@ -278,6 +292,29 @@ SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, UDERA>& A, SpParMat<
                                            bool clearA = false, bool clearB = false, int exec = CBG_EXEC_PANEL) {
   return detail::summa<SR, NUO, UDERO>(A, B, CBG_SYNCH, clearA, clearB, exec);
 }
+// ParFriends.h:449-451 signature.  Phases cut B's local tile by columns and C is
+// column-concatenated; the Markov-clustering pruning arguments must keep their
+// no-pruning values (hardThreshold, selectNum, recoverNum, recoverPct <= 0),
+// kselectVersion/computationKernel/perProcessMemory are accepted and unused.
+template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2, typename UDERA,
+          typename UDERB>
+SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B, int phases,
+                                             NUO hardThreshold, IU selectNum, IU recoverNum, NUO recoverPct,
+                                             int kselectVersion, int computationKernel, int64_t perProcessMemory) {
+  (void)kselectVersion;
+  (void)computationKernel;
+  (void)perProcessMemory;
+  if (hardThreshold > 0 || selectNum > 0 || recoverNum > 0 || recoverPct > 0)
+    cbg_abort_on(CBG_ERR_INVALIDPARAMS, "MemEfficientSpGEMM: pruning is not supported");
+  if (A.getncol() != B.getnrow()) cbg_abort_on(CBG_ERR_DIMMISMATCH, "Can not multiply, dimensions does not match");
+  cbg_tile c{};
+  cbg_abort_on(cbg_summa_spgemm_phased(A.commGrid->handle(), A.spSeq->tile(), B.spSeq->tile(), A.getncol(),
+                                       B.getnrow(), SR::code, CBG_DOUBLEBUFF, CBG_EXEC_PANEL, phases, nullptr,
+                                       nullptr, &c),
+               "MemEfficientSpGEMM");
+  return SpParMat<IU, NUO, UDERO>(new UDERO(c), A.commGrid, A.getnrow(), B.getncol());
+}
+
 // SpParMat.h:454-467
 template <typename SR, typename IU, typename NU1, typename NU2, typename UDERA, typename UDERB>
 SpParMat<IU, typename SR::T_promote, UDERA> PSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B) {

@@ -90,6 +90,12 @@ int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* left, cbg_tile
 int cbg_tile_split_rows(const cbg_tile* t, int64_t cut, cbg_tile* top, cbg_tile* bottom);
 /* structural + value digest (same definition as tests/golden/make_golden.py), device tile */
 int cbg_tile_digest(const cbg_tile* t, int64_t row_off, int64_t col_off, uint64_t* hs, uint64_t* hv, double* vsum);
+/* SpDCCols::operator== (SpDCCols.h:74-81, Dcsc::operator== dcsc.cpp:472-510):
+ * two empty tiles are equal; else m, n, nnz, nzc, cp, jc, ir must match and
+ * values be ErrorTolerantEqual (Compare.h:47-65: equal, or absolute or
+ * relative difference < epsilon; the reference's EPSILON is 0.01, SpDefs.h:64).
+ * Device tiles; *equal receives 1 or 0. */
+int cbg_tile_equal(const cbg_tile* a, const cbg_tile* b, double epsilon, int* equal);
 
 /* ---------------- generator ---------------- */
 /* Graph500 Kronecker R-MAT as DistEdgeList::GenGraph500Data(packed, scrambled)
@@ -148,6 +154,23 @@ int cbg_grid_allreduce_sum_i64(cbg_grid* g, int64_t* value);
  * C_local receives this rank's tile C(prow,pcol). */
 int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
                      int64_t B_gnrow, int semiring, int algo, int exec, cbg_tile* C_local);
+
+/* MemEfficientSpGEMM (ParFriends.h:449-730) without its Markov-clustering
+ * pruning: this rank's B tile is cut into `phases` column pieces
+ * (SpDCCols::ColSplit, SpDCCols.cpp:936-970: cuts at (i+1)*(n/phases)), each
+ * piece goes through the SUMMA above, and the phase results are
+ *   fn == NULL: column-concatenated on device into C_local
+ *               (SpDCCols::ColConcatenate, ParFriends.h:724-725);
+ *   fn != NULL: handed to fn(user, phase, col_offset, C_phase) one at a time
+ *               and freed after the call (C streamed when it does not fit HBM;
+ *               C_local may be NULL).  fn runs on every rank between the
+ *               collectives; a nonzero return is reported after all phases.
+ * phases < 1 or >= A_gncol is reset to 1 (ParFriends.h:469-473).  Every rank
+ * needs B_local->n >= phases (CBG_ERR_INVALIDPARAMS otherwise, collectively). */
+typedef int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg_tile* C_phase);
+int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
+                            int64_t B_gnrow, int semiring, int algo, int exec, int phases, cbg_phase_fn fn,
+                            void* user, cbg_tile* C_local);
 
 #ifdef __cplusplus
 }

@@ -106,6 +106,25 @@ def main():
                 print(algo, ex, "OK" if good else f"BAD {tot} vs {gd}", flush=True)
             ok = ok and good
             C.tile.free()
+    # MemEfficientSpGEMM phases: concatenated result equals the unphased one
+    # (SpParMat::operator==, AND over the grid), streamed phases add up to it
+    import pickle
+    C1 = cbg.Mult_AnXBn_DoubleBuff(Ad, Bd)
+    Cp = cbg.MemEfficientSpGEMM(Ad, Bd, 3)
+    same = (Cp == C1)
+    r0, _ = cbg.block_range(A["m"], pr, grid.prow)
+    c0, _ = cbg.block_range(B["n"], pc, grid.pcol)
+    parts = []
+    cbg.MemEfficientSpGEMM(Ad, Bd, 3, on_phase=lambda ph, off, t: parts.append(t.digest(r0, c0 + off)))
+    mine = add_digests(parts)
+    alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(mine))))]
+    tot = add_digests(alld)
+    good = same and tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"]
+    if rank == 0:
+        print("phased", "OK" if good else f"BAD same={same} {tot} vs {gd}", flush=True)
+    ok = ok and good
+    C1.tile.free()
+    Cp.tile.free()
     grid.destroy()
     dist.barrier()
     if rank == 0 and ok:

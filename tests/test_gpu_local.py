@@ -221,3 +221,77 @@ print(json.dumps(out))
         g = G["rmat"][f"s{scale}_ef16"]["C_local_plus"]
         assert d["nnz"] == g["nnz"] and d["hs"] == g["hs"] and d["hv"] == g["hv"], (env, scale)
         assert d["n_big"] > 0
+
+
+def _self_grid(cbg):
+    class Self:
+        def bcast(self, comm, arr, root):
+            pass
+
+        def allgather(self, comm, data):
+            return data
+
+    return cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+
+
+def test_tile_equal_semantics(cbg):
+    """SpDCCols::operator== / ErrorTolerantEqual (EPSILON 0.01, SpDefs.h:64)."""
+    d = load_npz("rmat_s10_ef16_A.npz")
+    A = cbg.Tile.from_dict(d)
+    assert A == cbg.Tile.from_dict(d)
+    v = d["val"].copy()
+    v[5] *= 1.005                      # relative error 0.5 % < 1 %
+    assert A == cbg.Tile.from_dict(dict(d, val=v))
+    v[5] = d["val"][5] * 1.02          # 2 % > 1 %, and |diff| >= 0.01
+    assert not A == cbg.Tile.from_dict(dict(d, val=v))
+    assert A.equal(cbg.Tile.from_dict(dict(d, val=v)), epsilon=0.05)
+    v = d["val"].copy()
+    v[7] = np.nan
+    assert not A == cbg.Tile.from_dict(dict(d, val=v))
+    ir = d["ir"].copy()
+    ir[0] += 1 if ir[1] > ir[0] + 1 else 0
+    if not np.array_equal(ir, d["ir"]):
+        assert not A == cbg.Tile.from_dict(dict(d, ir=ir))
+    z0 = cbg.Tile.from_host(3, 4, np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    z1 = cbg.Tile.from_host(5, 6, np.zeros(1, np.int64), np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0))
+    assert z0 == z1                    # both empty: equal whatever the shape (SpDCCols.h:76-77)
+    assert not A == z0
+
+
+@pytest.mark.parametrize("phases", [1, 2, 3, 7, 1024])
+def test_phased_spgemm_matches_reference(cbg, phases):
+    """MemEfficientSpGEMM phases (ColSplit + ColConcatenate) vs the reference's product."""
+    g = _self_grid(cbg)
+    A = cbg.SpParMat.rmat(g, 10)
+    B = cbg.SpParMat.rmat(g, 10)
+    C = cbg.MemEfficientSpGEMM(A, B, phases)   # phases >= ncol resets to 1 (ParFriends.h:469-473)
+    assert_tiles_equal(C.tile.to_host(), load_npz("rmat_s10_ef16_C_local_plus.npz"))
+    Cm = cbg.MemEfficientSpGEMM(A, B, phases, sr="minplus")
+    assert_tiles_equal(Cm.tile.to_host(), load_npz("rmat_s10_ef16_C_local_minplus.npz"))
+    Calias = cbg.MemEfficientSpGEMM(A, A, phases)  # allowed: the reference copies B
+    assert Calias == C
+    g.destroy()
+
+
+def test_phased_spgemm_streamed(cbg):
+    """on_phase streaming: phase tiles with their column offsets add up to the full digest."""
+    g = _self_grid(cbg)
+    A = cbg.SpParMat.rmat(g, 12)
+    B = cbg.SpParMat.rmat(g, 12)
+    seen = []
+    cbg.MemEfficientSpGEMM(A, B, 5, on_phase=lambda p, off, t: seen.append((p, off, t.n, t.digest(0, off))))
+    assert [s[0] for s in seen] == list(range(5))
+    w = 4096 // 5
+    assert [s[1] for s in seen] == [p * w for p in range(5)]
+    assert [s[2] for s in seen] == [w] * 4 + [4096 - 4 * w]
+    hs = sum(int(s[3]["hs"], 16) for s in seen) % (1 << 64)
+    hv = sum(int(s[3]["hv"], 16) for s in seen) % (1 << 64)
+    gd = golden()["rmat"]["s12_ef16"]["C_local_plus"]
+    assert sum(s[3]["nnz"] for s in seen) == gd["nnz"]
+    assert "%016x" % hs == gd["hs"] and "%016x" % hv == gd["hv"]
+    with pytest.raises(ValueError):
+        cbg.MemEfficientSpGEMM(A, B, 2, on_phase=lambda p, off, t: (_ for _ in ()).throw(ValueError("x")))
+    with pytest.raises(cbg.CbgError) as e:
+        cbg.MemEfficientSpGEMM(A, B, 2, hardThreshold=0.5)
+    assert e.value.code == cbg.INVALIDPARAMS
+    g.destroy()

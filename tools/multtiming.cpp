@@ -108,6 +108,14 @@ int main(int argc, char* argv[]) {
       std::printf("Synchronous multiplications finished\n");
       std::printf("%.6lf seconds elapsed per iteration\n", (t2 - t1) / (double)ITERATIONS);
     }
+    {
+      // MemEfficientSpGEMM with 4 phases (ParFriends.h:449) must equal the
+      // unphased product (SpParMat::operator==, SpParMat.cpp:2878)
+      PMat C = Mult_AnXBn_Synch<PTDOUBLEDOUBLE, double, DCCols>(A, B);
+      PMat Cp = MemEfficientSpGEMM<PTDOUBLEDOUBLE, double, DCCols>(A, B, 4, 0.0, 0, 0, 0.0, 1, 1, 0);
+      const bool same = (C == Cp);
+      if (myrank == 0) std::printf("MemEfficientSpGEMM (4 phases) %s the unphased product\n", same ? "equals" : "DIFFERS from");
+    }
   }
   MPI_Finalize();
   return 0;
