@@ -1,15 +1,18 @@
 #!/usr/bin/env python3
 """bench.py -- nnz(C)/s of R-MAT A*A through the MI355X 2D-SUMMA SpGEMM path.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--algo doublebuff|synch]
-                  [--exec panel|staged] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--phases P]
+                  [--algo doublebuff|synch] [--exec panel|staged] [--no-cpu-baseline]
 
 One step = one complete Mult_AnXBn_DoubleBuff (reference ParFriends.h:798-997)
 of Graph500 R-MAT A (SEED 0xDECAFBAD, ef 16, duplicates summed, loops removed)
-by a deep copy of A, inputs resident in HBM in the 2D block layout, C left
-resident per tile.  N=1 runs the largest configuration that fits one GPU
-(configs[1]: scale 18 by default).  N>1: launched by torch.distributed.run, one
-rank per GPU, RCCL row/column communicators (grid 2x1, 2x2, 4x2 for 2/4/8).
+by a deep copy of A, inputs resident in HBM in the 2D block layout.  Every N
+runs the metric's scale 22.  N=1: C (297 GB) exceeds one GPU's HBM, so the
+multiply runs as MemEfficientSpGEMM with 4 B-column phases (ParFriends.h:449),
+each phase's C materialized in HBM and released; N>1: C left resident per
+tile.  N>1 is launched by torch.distributed.run, one rank per GPU, RCCL
+row/column communicators (grid 2x1, 2x2, 4x2 for 2/4/8).  --scale 18 gives
+configs[1] (C resident on one GPU).
 
 Prints ONE JSON line on rank 0 (see the driver contract in DESIGN.md).
 """
@@ -51,22 +54,28 @@ def parse():
     p.add_argument("--seed", type=lambda s: int(s, 0), default=0xDECAFBAD)
     p.add_argument("--algo", choices=["doublebuff", "synch"], default="doublebuff")
     p.add_argument("--exec", dest="exec_mode", choices=["panel", "staged"], default="panel")
+    p.add_argument("--phases", type=int, default=None,
+                   help="MemEfficientSpGEMM phases (B column pieces); >1 streams C per phase "
+                        "(for C larger than HBM, e.g. scale 22 on one GPU)")
+    p.add_argument("--phase-consumer", choices=["none", "digest"], default="none",
+                   help="what the phase callback does with each phase's device C tile")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-scale", type=int, default=None, help="scale of the CPU-baseline sample")
     return p.parse_args()
 
 
-def pmc_traffic(scale, ef):
-    """HBM bytes of one local multiply at this scale from the committed PMC passes
-    (profiles/<round>_traffic_s<scale>.json, made by tools/profile_round.sh +
-    tools/traffic.py: FETCH_SIZE calibrated on k_digest, + WRITE_SIZE), or None."""
+def pmc_traffic(scale, ef, phases):
+    """HBM bytes of one local multiply (all phases) at this configuration from the
+    committed PMC passes (profiles/<round>_traffic_s<scale>.json, made by
+    tools/profile_round.sh + tools/traffic.py: FETCH_SIZE calibrated on k_digest,
+    + WRITE_SIZE), or None."""
     path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (ROUND, scale))
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    if d.get("scale") != scale or d.get("ef") != ef:
+    if d.get("scale") != scale or d.get("ef") != ef or d.get("phases", 1) != phases:
         return None, None
     return d["traffic_bytes"], os.path.relpath(path, REPO)
 
@@ -101,7 +110,9 @@ def main():
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     N = max(world, 1)
-    scale = a.scale if a.scale is not None else (18 if N == 1 else 22)
+    scale = a.scale if a.scale is not None else 22
+    if a.phases is None:
+        a.phases = 4 if (N == 1 and scale >= 21) else 1
     cbg = load_cbg()  # libcbg first: its HIP/RCCL runtimes are the ones the process uses
     cbg.lib().cbg_set_device(local_rank % max(1, cbg.device_count()))
 
@@ -144,10 +155,29 @@ def main():
     mult = cbg.Mult_AnXBn_DoubleBuff if a.algo == "doublebuff" else cbg.Mult_AnXBn_Synch
     exec_mode = cbg.EXEC_PANEL if a.exec_mode == "panel" else cbg.EXEC_STAGED
 
+    algo = cbg.DOUBLEBUFF if a.algo == "doublebuff" else cbg.SYNCH
+
+    def step():
+        """one complete multiply; returns (local nnz(C), resident C or None)"""
+        if a.phases <= 1:
+            C = mult(A, B, exec_mode=exec_mode)
+            return C.tile.nnz, C
+        seen = [0]
+
+        def consume(phase, off, t):  # C of one phase, resident until this returns
+            seen[0] += t.nnz
+            if a.phase_consumer == "digest":
+                t.digest(0, off)
+
+        cbg.MemEfficientSpGEMM(A, B, a.phases, algo=algo, exec_mode=exec_mode, on_phase=consume)
+        return seen[0], None
+
     C = None
     for _ in range(a.warmup):
-        C = mult(A, B, exec_mode=exec_mode)
-        C.tile.free()
+        _, C = step()
+        if C is not None:
+            C.tile.free()
+            C = None
     grid.barrier()
     cbg.synchronize()
     ms_local = []
@@ -155,14 +185,14 @@ def main():
     for _ in range(a.steps):
         if C is not None:
             C.tile.free()
-        C = mult(A, B, exec_mode=exec_mode)
+        nnz_local, C = step()
         st = cbg.last_stats()
         ms_local.append(st["ms_symbolic"] + st["ms_numeric"])
     cbg.synchronize()
     grid.barrier()
     dt = time.perf_counter() - t0
     dt = grid.allreduce_max(dt)
-    nnz_c = grid.allreduce_sum(C.tile.nnz)
+    nnz_c = grid.allreduce_sum(nnz_local)
     st = cbg.last_stats()
     flops = grid.allreduce_sum(st["flops"])
     # algorithmic bytes of the local multiply: 16F + 12 nnz(C) + 32 nnz(B) + 8 n
@@ -173,7 +203,7 @@ def main():
     achieved = grid.allreduce_max(achieved) if N > 1 else achieved
 
     if rank == 0:
-        traffic, traffic_src = pmc_traffic(scale, a.ef) if N == 1 else (None, None)
+        traffic, traffic_src = pmc_traffic(scale, a.ef, a.phases) if N == 1 else (None, None)
         out = {
             "metric": "nnz(C)/sec for A·A (R-MAT scale %d) at %d GPUs" % (scale, N),
             "value": nnz_c * a.steps / dt,
@@ -183,8 +213,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": dt / a.steps * 1e3,
             "higher_is_better": True,
-            # N>=2 multiply the same scale-22 problem (total work fixed); N=1 runs scale 18
-            # because C of scale 22 (297 GB) exceeds one GPU's HBM
+            # every N multiplies the same scale-22 problem (total work fixed)
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
@@ -193,7 +222,10 @@ def main():
                 scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
-                "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport},
+                "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport,
+                "phases": a.phases,
+                "C": "resident in HBM" if a.phases <= 1 else
+                     "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
@@ -209,7 +241,8 @@ def main():
                                    "sample": "R-MAT scale-%d ef%d A*A, oracle Mult_AnXBn_%s 1x1, %.1f s" % (
                                        cs, a.ef, algo.capitalize(), cdt)}
         print(json.dumps(out), flush=True)
-    C.tile.free()
+    if C is not None:
+        C.tile.free()
     grid.destroy()
 
 
