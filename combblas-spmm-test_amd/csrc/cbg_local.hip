@@ -327,8 +327,11 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   int* st = pref + BS + 4;
   int* tmp = st + BS;
   const int tid = threadIdx.x;
-  const int br = blockIdx.x;
-  const int b = br / R, r = br % R;
+  // panel-major block order: the blocks in flight gather A's panel-r segments
+  // (~1/R of A), which then stay in L2 / Infinity Cache
+  const int nbig = (int)(gridDim.x / R);
+  const int r = blockIdx.x / nbig, b = blockIdx.x % nbig;
+  const int br = b * R + r;
   const int col = perm_big[b];
   const int R0 = r << plog;
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), m);
@@ -525,11 +528,19 @@ __device__ __forceinline__ int slab_class(int w, int small_cap) {
   }
   return w <= small_cap ? 0 : 1;
 }
-// pass 1: within-panel -> within-column offsets, class counts
+// The slab list is ordered by (class, panel): a class is one launch, and
+// inside it the slabs of panel r run together, so the A rows they gather
+// (A's panel-r segments, ~1/R of A) stay in L2 / Infinity Cache.  key = c *
+// KR + r with KR = R (KR = 1, class order only, if the keys overflow LDS).
+constexpr int SLAB_KEYS_MAX = 8192;
+__host__ __device__ inline int slab_kr(int R) { return SLAB_NCLS * R <= SLAB_KEYS_MAX ? R : 1; }
+
+// pass 1: within-panel -> within-column offsets, (class, panel) counts
 __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
                              int4* __restrict__ desc, int small_cap, int* __restrict__ counts) {
-  __shared__ int lc[SLAB_NCLS];
-  if (threadIdx.x < SLAB_NCLS) lc[threadIdx.x] = 0;
+  extern __shared__ int lc[];  // [SLAB_NCLS * KR]
+  const int KR = slab_kr(R), NK = SLAB_NCLS * KR;
+  for (int k = threadIdx.x; k < NK; k += blockDim.x) lc[k] = 0;
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < nbig) {
@@ -539,55 +550,57 @@ __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab,
       for (int s = 0; s < nslab[br]; ++s) {
         int4& d = desc[(int64_t)br * NFINE_MAX + s];
         d.z += off;
-        atomicAdd(&lc[slab_class(d.w, small_cap)], 1);
+        atomicAdd(&lc[slab_class(d.w, small_cap) * KR + (KR > 1 ? r : 0)], 1);
       }
       off += cnt_br[br];
     }
   }
   __syncthreads();
-  if (threadIdx.x < SLAB_NCLS && lc[threadIdx.x]) atomicAdd(&counts[threadIdx.x], lc[threadIdx.x]);
+  for (int k = threadIdx.x; k < NK; k += blockDim.x)
+    if (lc[k]) atomicAdd(&counts[k], lc[k]);
 }
-// class bases (exclusive prefix of the counts) into cursor[]
-__global__ void k_slab_bases(const int* __restrict__ counts, int* __restrict__ cursor) {
+// key bases (exclusive prefix of the counts) into cursor[], class totals into cls[]
+__global__ void k_slab_bases(int R, const int* __restrict__ counts, int* __restrict__ cursor, int* __restrict__ cls) {
   if (threadIdx.x == 0) {
+    const int KR = slab_kr(R);
     int s = 0;
     for (int c = 0; c < SLAB_NCLS; ++c) {
-      cursor[c] = s;
-      s += counts[c];
+      int t = 0;
+      for (int r = 0; r < KR; ++r) {
+        cursor[c * KR + r] = s;
+        s += counts[c * KR + r];
+        t += counts[c * KR + r];
+      }
+      cls[c] = t;
     }
   }
 }
-// pass 2: slab records into their class segment of one list
+// pass 2: slab records into their (class, panel) segment of one list
 __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, const int4* __restrict__ desc,
                             int small_cap, int* __restrict__ cursor, SlabRec* __restrict__ list,
                             const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
                             const int64_t* __restrict__ colptr, const int* __restrict__ gbm_slot, int plog,
                             int64_t m_rows) {
-  __shared__ int lc[SLAB_NCLS], lb[SLAB_NCLS];
-  if (threadIdx.x < SLAB_NCLS) lc[threadIdx.x] = 0;
+  extern __shared__ int lsh[];  // lc[NK] | lb[NK]
+  const int KR = slab_kr(R), NK = SLAB_NCLS * KR;
+  int* lc = lsh;
+  int* lb = lsh + NK;
+  for (int k = threadIdx.x; k < NK; k += blockDim.x) lc[k] = 0;
   __syncthreads();
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  int mine[SLAB_NCLS];
-#pragma unroll
-  for (int c = 0; c < SLAB_NCLS; ++c) mine[c] = 0;
   if (b < nbig)
     for (int r = 0; r < R; ++r) {
       const int br = b * R + r;
-      for (int s = 0; s < nslab[br]; ++s) {
-        const int c = slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap);
-#pragma unroll
-        for (int q = 0; q < SLAB_NCLS; ++q) mine[q] += (q == c);
-      }
+      for (int s = 0; s < nslab[br]; ++s)
+        atomicAdd(&lc[slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap) * KR + (KR > 1 ? r : 0)], 1);
     }
-  int o[SLAB_NCLS];
-#pragma unroll
-  for (int c = 0; c < SLAB_NCLS; ++c) o[c] = mine[c] ? atomicAdd(&lc[c], mine[c]) : 0;
   __syncthreads();
-  if (threadIdx.x < SLAB_NCLS && lc[threadIdx.x]) lb[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], lc[threadIdx.x]);
+  for (int k = threadIdx.x; k < NK; k += blockDim.x) {
+    lb[k] = lc[k] ? atomicAdd(&cursor[k], lc[k]) : 0;
+    lc[k] = 0;
+  }
   __syncthreads();
   if (b >= nbig) return;
-#pragma unroll
-  for (int c = 0; c < SLAB_NCLS; ++c) o[c] += lb[c];
   const int col = perm_big[b];
   const int64_t p0 = cpB[col], nb = cpB[col + 1] - p0, cbase = colptr[col];
   for (int r = 0; r < R; ++r) {
@@ -596,7 +609,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
     const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
     for (int s = 0; s < nslab[br]; ++s) {
       const int4 d = desc[(int64_t)br * NFINE_MAX + s];
-      const int c = slab_class(d.w, small_cap);
+      const int key = slab_class(d.w, small_cap) * KR + (KR > 1 ? r : 0);
       SlabRec rec;
       rec.obase = cbase + d.z;
       rec.p0 = p0;
@@ -608,9 +621,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
       rec.slot = gbm_slot ? gbm_slot[br] : -1;
       rec.full = (d.x == R0 && d.y == R1);
       rec.pad = 0;
-#pragma unroll
-      for (int q = 0; q < SLAB_NCLS; ++q)
-        if (q == c) list[o[q]++] = rec;
+      list[lb[key] + atomicAdd(&lc[key], 1)] = rec;
     }
   }
 }
@@ -1535,15 +1546,17 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   int ncls[SLAB_NCLS] = {};
   if (nbig > 0 && nslabs > 0) {
     slist.reset(nslabs);
-    DBuf<int> counters(2 * SLAB_NCLS);
-    CBG_HIP(hipMemsetAsync(counters.p, 0, 2 * SLAB_NCLS * sizeof(int), s));
-    hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.cnt_br.p,
-                       bp.desc.p, SLAB_SMALL_CAP, counters.p);
-    hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, counters.p, counters.p + SLAB_NCLS);
-    hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 0, s, nbig, bp.R, bp.nslab.p, bp.desc.p,
-                       SLAB_SMALL_CAP, counters.p + SLAB_NCLS, slist.p, bp.perm_big, B.cp, colptr.p, bp.gbm_slot.p,
-                       bp.plog, A.m);
-    CBG_HIP(hipMemcpyAsync(ncls, counters.p, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
+    const int NK = SLAB_NCLS * slab_kr(bp.R);
+    DBuf<int> counters(2 * NK + SLAB_NCLS);  // counts[NK] | cursor[NK] | class totals
+    CBG_HIP(hipMemsetAsync(counters.p, 0, (2 * NK + SLAB_NCLS) * sizeof(int), s));
+    hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), NK * sizeof(int), s, nbig, bp.R, bp.nslab.p,
+                       bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, counters.p);
+    hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, bp.R, counters.p, counters.p + NK,
+                       counters.p + 2 * NK);
+    hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 2 * NK * sizeof(int), s, nbig, bp.R,
+                       bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, counters.p + NK, slist.p, bp.perm_big, B.cp, colptr.p,
+                       bp.gbm_slot.p, bp.plog, A.m);
+    CBG_HIP(hipMemcpyAsync(ncls, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
