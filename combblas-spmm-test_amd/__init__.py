@@ -568,12 +568,86 @@ class SpParMat:
         return SpParMat(t, grid, nv, nv)
 
     @staticmethod
+    def ParallelReadMM(grid, filename, onebased=True, binop="max"):
+        """SpParMat::ParallelReadMM (SpParMat.cpp:3980-4117): every rank parses the
+        file and keeps its block of the block distribution (the reference splits
+        the byte range across ranks and redistributes with Alltoallv; the
+        resulting tiles are the same)."""
+        return SpParMat.from_global(grid, read_mm(filename, onebased, binop))
+
+    @staticmethod
     def from_global(grid, d):
         """Distribute a global host DCSC dict by the block distribution (SpParMat::Owner)."""
         r0, r1 = block_range(d["m"], grid.grid_rows, grid.prow)
         c0, c1 = block_range(d["n"], grid.grid_cols, grid.pcol)
         t = sub_tile(d, r0, r1, c0, c1)
         return SpParMat(Tile.from_dict(t), grid, d["m"], d["n"])
+
+
+_BINOPS = {"max": np.maximum, "min": np.minimum, "plus": np.add, "first": None}
+
+
+def read_mm(path, onebased=True, binop="max"):
+    """Matrix Market coordinate file -> global host DCSC dict, with the semantics of
+    SpParMat::ParallelReadMM (SpParMat.cpp:3980-4117): real / integer / pattern
+    (value 1), symmetric or hermitian entries mirrored (SpHelper::push_to_vectors,
+    SpHelper.h:75-91), duplicates combined with BinOp after a column-major sort
+    (SpTuples::RemoveDuplicates; the reference's MultTest uses maximum<double>)."""
+    with open(path) as f:
+        banner = f.readline().split()
+        if len(banner) < 5 or banner[0].lower() != "%%matrixmarket" or banner[2].lower() != "coordinate":
+            raise CbgError(INVALIDPARAMS, f"{path}: not a Matrix Market coordinate file")
+        field, sym = banner[3].lower(), banner[4].lower()
+        if field not in ("real", "integer", "pattern", "double"):
+            raise CbgError(INVALIDPARAMS, f"{path}: unsupported Matrix Market field '{field}'")
+        line = f.readline()
+        while line.startswith("%") or not line.strip():
+            line = f.readline()
+        m, n, nz = (int(x) for x in line.split()[:3])
+        data = np.loadtxt(f, ndmin=2) if nz else np.zeros((0, 3))
+    rows = data[:, 0].astype(np.int64)
+    cols = data[:, 1].astype(np.int64)
+    vals = np.ones(len(rows)) if field == "pattern" else data[:, 2].astype(np.float64)
+    if onebased:
+        rows, cols = rows - 1, cols - 1
+    if sym in ("symmetric", "hermitian"):
+        off = rows != cols
+        rows, cols, vals = (np.concatenate([rows, cols[off]]), np.concatenate([cols, rows[off]]),
+                            np.concatenate([vals, vals[off]]))
+    order = np.lexsort((rows, cols))
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    if len(rows):
+        first = np.ones(len(rows), bool)
+        first[1:] = (rows[1:] != rows[:-1]) | (cols[1:] != cols[:-1])
+        starts = np.flatnonzero(first)
+        op = _BINOPS[binop] if isinstance(binop, str) else binop
+        if op is None:
+            vals = vals[starts]
+        elif isinstance(op, np.ufunc):
+            vals = op.reduceat(vals, starts)
+        else:
+            ends = np.append(starts[1:], len(vals))
+            out = []
+            for a, b in zip(starts, ends):
+                v = vals[a]
+                for x in vals[a + 1:b]:
+                    v = op(v, x)
+                out.append(v)
+            vals = np.asarray(out, np.float64)
+        rows, cols = rows[starts], cols[starts]
+    jc, start = np.unique(cols, return_index=True)
+    cp = np.append(start, len(rows)).astype(np.int64)
+    return dict(m=m, n=n, cp=cp, jc=jc.astype(np.int32), ir=rows.astype(np.int32), val=vals.astype(np.float64))
+
+
+def write_mm(path, d):
+    """global host DCSC dict -> Matrix Market coordinate real general (1-based)."""
+    cols = np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"]))
+    with open(path, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n")
+        f.write(f"{d['m']} {d['n']} {len(d['ir'])}\n")
+        for r, c, v in zip(d["ir"], cols, d["val"]):
+            f.write(f"{int(r) + 1} {int(c) + 1} {float(v)!r}\n")
 
 
 def sub_tile(d, r0, r1, c0, c1):

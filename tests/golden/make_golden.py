@@ -167,7 +167,26 @@ def main():
 
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(gold, f, indent=1, sort_keys=True)
+    multtest_fixture()
+
+
+def multtest_fixture():
+    """ReleaseTests/MultTest inputs: the reference's bundled sevenvertex.mtx (data
+    file, copied) and CControl = the reference's product of it with itself
+    (sevenvertex_C_local_plus.npz above), written as Matrix Market."""
+    import shutil
+    shutil.copyfile(f"{REF}/ReleaseTests/sevenvertex.mtx", os.path.join(HERE, "sevenvertex.mtx"))
+    d = np.load(os.path.join(HERE, "sevenvertex_C_local_plus.npz"))
+    cols = np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"]))
+    with open(os.path.join(HERE, "sevenvertex_C.mtx"), "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n")
+        f.write(f"{int(d['m'])} {int(d['n'])} {len(d['ir'])}\n")
+        for r, c, v in zip(d["ir"], cols, d["val"]):
+            f.write(f"{int(r) + 1} {int(c) + 1} {float(v)!r}\n")
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "multtest":
+        multtest_fixture()
+    else:
+        main()

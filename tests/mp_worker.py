@@ -45,6 +45,21 @@ def main():
         dist.init_process_group("gloo")
         hc = cbg.GlooHostComm(pr, pc)
     G = golden()
+    if case == "multtest":
+        # ReleaseTests/MultTest.cpp SpGEMM part on a pr x pc grid: ParallelReadMM of
+        # A, B, CControl; Synch / DoubleBuff / phased products == CControl
+        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        mm = os.path.join(HERE, "golden", "sevenvertex.mtx")
+        A = cbg.SpParMat.ParallelReadMM(grid, mm)
+        B = cbg.SpParMat.ParallelReadMM(grid, mm)
+        CC = cbg.SpParMat.ParallelReadMM(grid, os.path.join(HERE, "golden", "sevenvertex_C.mtx"))
+        ok = (cbg.Mult_AnXBn_Synch(A, B) == CC) and (cbg.Mult_AnXBn_DoubleBuff(A, B) == CC)
+        ok = ok and (cbg.MemEfficientSpGEMM(A, B, 2) == CC)
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if ok else "MULTTEST FAILED", flush=True)
+        return
     if case.startswith("rmat"):
         A = load_npz("rmat_s10_ef16_A.npz")
         B = A

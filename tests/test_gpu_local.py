@@ -295,3 +295,18 @@ def test_phased_spgemm_streamed(cbg):
         cbg.MemEfficientSpGEMM(A, B, 2, hardThreshold=0.5)
     assert e.value.code == cbg.INVALIDPARAMS
     g.destroy()
+
+
+def test_multtest_sevenvertex(cbg):
+    """ReleaseTests/MultTest.cpp:95-180 SpGEMM part: ParallelReadMM of A, B and
+    CControl, then Synch and DoubleBuff must equal CControl (SpParMat::operator==)."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    g = _self_grid(cbg)
+    A = cbg.SpParMat.ParallelReadMM(g, os.path.join(gold, "sevenvertex.mtx"), True, "max")
+    B = cbg.SpParMat.ParallelReadMM(g, os.path.join(gold, "sevenvertex.mtx"), True, "max")
+    CControl = cbg.SpParMat.ParallelReadMM(g, os.path.join(gold, "sevenvertex_C.mtx"), True, "max")
+    assert cbg.Mult_AnXBn_Synch(A, B) == CControl
+    assert cbg.Mult_AnXBn_DoubleBuff(A, B) == CControl
+    assert cbg.MemEfficientSpGEMM(A, B, 2) == CControl
+    g.destroy()

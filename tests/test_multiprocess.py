@@ -46,3 +46,11 @@ def test_host_transport_cpu(grid, case, transport):
 def test_summa_multiprocess_gpu(grid, case):
     rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), case], timeout=600)
     assert rc == 0 and "MPOK" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2)])
+def test_multtest_multiprocess_gpu(grid):
+    """MultTest's SpGEMM checks (ParallelReadMM + operator== against CControl) on a grid."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "multtest"], timeout=600)
+    assert rc == 0 and "MPOK" in out, out[-3000:]
