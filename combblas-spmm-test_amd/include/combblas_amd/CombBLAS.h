@@ -18,6 +18,7 @@
 // reference MPI_Aborts on (DIMMISMATCH 3002, MATRIXALIAS 3005, NOTSQUARE 3003)
 // aborts here with the same code.  Define CBG_NO_MPI to use a single-process grid.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +50,12 @@ inline void cbg_abort_on(int rc, const char* what) {
 }
 
 // ---------------------------------------------------------------- semirings
+// Operations.h maximum<T> (the BinOp MultTest passes to ParallelReadMM)
+template <class T>
+struct maximum {
+  T operator()(const T& a, const T& b) const { return a < b ? b : a; }
+};
+
 template <class T1, class T2>
 struct PlusTimesSRing {
   typedef T1 T_promote;
@@ -200,6 +207,7 @@ template <class IT, class NT, class DER>
 class SpParMat {
  public:
   SpParMat() = default;
+  explicit SpParMat(std::shared_ptr<CommGrid> grid) : commGrid(grid) {}
   SpParMat(DER* seq, std::shared_ptr<CommGrid> grid, IT gm, IT gn) : spSeq(seq), commGrid(grid), m_(gm), n_(gn) {}
   SpParMat(SpParMat&& o) noexcept : spSeq(o.spSeq), commGrid(o.commGrid), m_(o.m_), n_(o.n_) { o.spSeq = nullptr; }
   SpParMat& operator=(SpParMat&& o) noexcept {
@@ -224,6 +232,60 @@ class SpParMat {
                  "rmat");
     const IT nv = (IT)1 << scale;
     return SpParMat(new DER(t), g, nv, nv);
+  }
+
+  // SpParMat::ParallelReadMM (SpParMat.cpp:3980-4117): Matrix Market coordinate
+  // real / integer / pattern (value 1), symmetric or hermitian entries mirrored
+  // (SpHelper::push_to_vectors, SpHelper.h:75-91), duplicates combined with BinOp
+  // in column-major order (SpTuples::RemoveDuplicates).  Every rank parses the
+  // file and keeps its block (the reference splits the bytes across ranks and
+  // redistributes; the tiles are the same).
+  template <typename BinOp>
+  void ParallelReadMM(const std::string& filename, bool onebased, BinOp binop) {
+    FILE* f = std::fopen(filename.c_str(), "r");
+    if (!f) cbg_abort_on(3004, ("Matrix-market file " + filename + " can not be found").c_str());  // NOFILE
+    char line[1024], mm[64], obj[64], fmt[64], field[64], sym[64];
+    if (!std::fgets(line, sizeof line, f) || std::sscanf(line, "%63s %63s %63s %63s %63s", mm, obj, fmt, field, sym) != 5 ||
+        std::strcmp(fmt, "coordinate") != 0)
+      cbg_abort_on(CBG_ERR_INVALIDPARAMS, "Could not process Matrix Market banner");
+    const bool pattern = std::strcmp(field, "pattern") == 0;
+    const bool symmetric = std::strcmp(sym, "symmetric") == 0 || std::strcmp(sym, "hermitian") == 0;
+    long long m = 0, n = 0, nz = 0;
+    while (std::fgets(line, sizeof line, f))
+      if (line[0] != '%' && std::sscanf(line, "%lld %lld %lld", &m, &n, &nz) == 3) break;
+    const int pr = commGrid->GetGridRows(), pc = commGrid->GetGridCols();
+    const int r = commGrid->GetRankInProcCol(), c = commGrid->GetRankInProcRow();
+    const long long mper = m / pr, nper = n / pc;  // SpParMat::Owner (SpParMat.cpp:5068-5097)
+    const long long r0 = r * mper, r1 = (r == pr - 1) ? m : r0 + mper;
+    const long long c0 = c * nper, c1 = (c == pc - 1) ? n : c0 + nper;
+    std::vector<std::tuple<IT, IT, NT>> t;
+    auto keep = [&](long long i, long long j, double v) {
+      if (i >= r0 && i < r1 && j >= c0 && j < c1) t.emplace_back((IT)(i - r0), (IT)(j - c0), (NT)v);
+    };
+    while (std::fgets(line, sizeof line, f)) {
+      long long i, j;
+      double v = 1.0;
+      const int got = pattern ? std::sscanf(line, "%lld %lld", &i, &j) : std::sscanf(line, "%lld %lld %lg", &i, &j, &v);
+      if (got < 2) continue;
+      if (onebased) { --i; --j; }
+      keep(i, j, v);
+      if (symmetric && i != j) keep(j, i, v);
+    }
+    std::fclose(f);
+    std::stable_sort(t.begin(), t.end(), [](const std::tuple<IT, IT, NT>& a, const std::tuple<IT, IT, NT>& b) {
+      return std::get<1>(a) != std::get<1>(b) ? std::get<1>(a) < std::get<1>(b) : std::get<0>(a) < std::get<0>(b);
+    });
+    std::vector<std::tuple<IT, IT, NT>> u;
+    for (auto& x : t) {
+      if (!u.empty() && std::get<0>(u.back()) == std::get<0>(x) && std::get<1>(u.back()) == std::get<1>(x))
+        std::get<2>(u.back()) = binop(std::get<2>(u.back()), std::get<2>(x));
+      else
+        u.push_back(x);
+    }
+    delete spSeq;
+    spSeq = new DER((IT)(r1 - r0), (IT)(c1 - c0), (IT)u.size(), u.data(), false);
+    m_ = (IT)m;
+    n_ = (IT)n;
   }
 
   IT getnrow() const { return m_; }

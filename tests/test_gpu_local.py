@@ -310,3 +310,21 @@ def test_multtest_sevenvertex(cbg):
     assert cbg.Mult_AnXBn_DoubleBuff(A, B) == CControl
     assert cbg.MemEfficientSpGEMM(A, B, 2) == CControl
     g.destroy()
+
+
+def test_cpp_multtest_driver():
+    """tools/multtest (C++ mirror header; built by __graft_entry__.build()) prints the
+    reference MultTest's success lines for the bundled sevenvertex inputs."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "tools", "multtest")
+    if not os.path.exists(exe):
+        pytest.skip("tools/multtest not built (needs MPICH in /opt/conda)")
+    g = os.path.join(repo, "tests", "golden")
+    r = subprocess.run([exe, os.path.join(g, "sevenvertex.mtx"), os.path.join(g, "sevenvertex.mtx"),
+                        os.path.join(g, "sevenvertex_C.mtx")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    for line in ("Synchronous Multiplication working correctly", "Double buffered multiplication working correctly",
+                 "Phased (MemEfficientSpGEMM) multiplication working correctly"):
+        assert line in r.stdout
