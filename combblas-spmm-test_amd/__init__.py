@@ -68,8 +68,12 @@ EXPORTS = [
     "cbg_tile_split_rows", "cbg_tile_digest", "cbg_rmat_tile", "cbg_local_spgemm", "cbg_local_symbolic", "cbg_merge",
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
-    "cbg_tile_equal", "cbg_summa_spgemm_phased",
+    "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
+    "cbg_grid_transpose",
 ]
+Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
+OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
+_OPS = {"multiplies": OP_MULTIPLIES, "plus": OP_PLUS, "min": OP_MIN, "max": OP_MAX}
 
 # int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg_tile* C_phase)
 PHASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p)
@@ -120,6 +124,10 @@ def lib():
         "cbg_summa_spgemm": ([vp, T, T, i64, i64, i32, i32, i32, T], i32),
         "cbg_tile_equal": ([T, T, ctypes.c_double, ctypes.POINTER(i32)], i32),
         "cbg_summa_spgemm_phased": ([vp, T, T, i64, i64, i32, i32, i32, i32, PHASE_FN, vp, T], i32),
+        "cbg_tile_transpose": ([T, T], i32),
+        "cbg_tile_dim_apply": ([T, i32, ctypes.POINTER(ctypes.c_double), i32], i32),
+        "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
+        "cbg_grid_transpose": ([vp, T, T], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -196,6 +204,20 @@ class Tile:
 
     __hash__ = object.__hash__
 
+    def transpose(self):
+        """SpDCCols::Transpose (SpDCCols.cpp:853-873) -> new device tile."""
+        t = Tile()
+        _check(lib().cbg_tile_transpose(ctypes.byref(self.c), ctypes.byref(t.c)))
+        return t
+
+    def dim_apply(self, dim, vec, op="multiplies"):
+        """SpParMat::DimApply on this tile (in place): vec has n (Column) or m (Row) values."""
+        v = np.ascontiguousarray(vec, np.float64)
+        if len(v) != (self.n if dim == Column else self.m):
+            raise CbgError(INVALIDPARAMS, "DimApply vector length does not match the tile")
+        _check(lib().cbg_tile_dim_apply(ctypes.byref(self.c), dim, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        _OPS.get(op, op)))
+
     def split_cols(self, cut):
         """SpDCCols::Split (SpDCCols.cpp:905-930)"""
         a, b = Tile(), Tile()
@@ -217,6 +239,14 @@ class Tile:
                 _lib.cbg_tile_free(ctypes.byref(self.c))
         except Exception:
             pass
+
+
+def restriction_tile(scale, order=2, seed=0x5EED, grid=(1, 1), pos=(0, 0)):
+    """Restriction operator tile (n x n/order, one nonzero per fine row, values in (0,1]),
+    the role of mfiles/genrestrict.m for the Galerkin driver."""
+    t = Tile()
+    _check(lib().cbg_restriction_tile(scale, order, seed, grid[0], grid[1], pos[0], pos[1], ctypes.byref(t.c)))
+    return t
 
 
 def rmat_tile(scale, edgefactor=16, seed=0xDECAFBAD, grid=(1, 1), pos=(0, 0)):
@@ -560,6 +590,40 @@ class SpParMat:
         return self.grid.allreduce_sum(1 - local) == 0
 
     __hash__ = object.__hash__
+
+    def Transpose(self):
+        """SpParMat::Transpose (SpParMat.cpp:3528-3590), in place; square grids only."""
+        t = Tile()
+        _check(lib().cbg_grid_transpose(self.grid.h, ctypes.byref(self.tile.c), ctypes.byref(t.c)))
+        self.tile.free()
+        self.tile, self.gm, self.gn = t, self.gn, self.gm
+
+    def DimApply(self, dim, vec, op="multiplies"):
+        """SpParMat::DimApply (SpParMat.cpp:801) with a dense global vector (host array of
+        ncol (Column) or nrow (Row) values); each rank applies its block's slice."""
+        total, parts, idx = ((self.gn, self.grid.grid_cols, self.grid.pcol) if dim == Column
+                             else (self.gm, self.grid.grid_rows, self.grid.prow))
+        lo, hi = block_range(total, parts, idx)
+        self.tile.dim_apply(dim, np.asarray(vec, np.float64)[lo:hi], op)
+
+    def __iadd__(self, other):
+        """SpParMat::operator+= (SpParMat.cpp:741): union, duplicates added (a MergeAll of the two tiles)."""
+        C = MergeAll([self.tile, other.tile], PlusTimesSRing)
+        self.tile.free()
+        self.tile = C
+        return self
+
+    def copy(self):
+        """deep copy (the reference's copy constructor)."""
+        a, b = self.tile.split_cols(self.tile.n)
+        b.free()
+        return SpParMat(a, self.grid, self.gm, self.gn)
+
+    @staticmethod
+    def restriction(grid, scale, order=2, seed=0x5EED):
+        n = 1 << scale
+        t = restriction_tile(scale, order, seed, (grid.grid_rows, grid.grid_cols), (grid.prow, grid.pcol))
+        return SpParMat(t, grid, n, n // order)
 
     @staticmethod
     def rmat(grid, scale, edgefactor=16, seed=0xDECAFBAD):

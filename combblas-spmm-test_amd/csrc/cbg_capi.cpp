@@ -22,6 +22,7 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
                  int exec, cbg_tile& C);
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                         int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C);
+int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out);
 }  // namespace cbg
 
 namespace {
@@ -180,6 +181,48 @@ int cbg_tile_equal(const cbg_tile* a, const cbg_tile* b, double epsilon, int* eq
   if (!equal || !(epsilon >= 0)) return fail(CBG_ERR_INVALIDPARAMS, "bad equality parameters");
   return guard([&] {
     *equal = cbg::tile_equal(*a, *b, epsilon, default_stream()) ? 1 : 0;
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_transpose(const cbg_tile* t, cbg_tile* out) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  if (!out) return fail(CBG_ERR_INVALIDPARAMS, "out is NULL");
+  return guard([&] {
+    cbg::tile_transpose(*t, *out, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_dim_apply(cbg_tile* t, int dim, const double* vec, int op) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  if ((dim != CBG_DIM_COLUMN && dim != CBG_DIM_ROW) || op < CBG_OP_MULTIPLIES || op > CBG_OP_MAX ||
+      (!vec && (dim == CBG_DIM_COLUMN ? t->n : t->m) > 0))
+    return fail(CBG_ERR_INVALIDPARAMS, "bad DimApply parameters");
+  return guard([&] {
+    cbg::tile_dim_apply(*t, dim, vec, op, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile* out) {
+  if (scale < 1 || scale > 30 || order < 1 || ((int64_t)1 << scale) / order < 1 || pr < 1 || pc < 1 || prow < 0 ||
+      prow >= pr || pcol < 0 || pcol >= pc || !out)
+    return fail(CBG_ERR_INVALIDPARAMS, "bad restriction parameters");
+  return guard([&] {
+    cbg::restriction_tile(scale, order, seed, pr, pc, prow, pcol, *out, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out) {
+  if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  if (int rc = check_tile(local, true, "tile")) return rc;
+  if (!out) return fail(CBG_ERR_INVALIDPARAMS, "out is NULL");
+  return guard([&]() -> int {
+    CBG_HIP(hipDeviceSynchronize());
+    int rc = cbg::grid_transpose(g, *local, *out);
+    if (rc) return fail(rc, "SpParMat::Transpose needs a square grid");
     return CBG_OK;
   });
 }

@@ -122,4 +122,10 @@ void tile_concat_rows(const std::vector<cbg_tile>& parts, const std::vector<int6
                       int64_t n, cbg_tile& out, hipStream_t s);
 bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s);
 
+// Galerkin path operations (cbg_ops.hip)
+void tile_transpose(const cbg_tile& T, cbg_tile& out, hipStream_t s);
+void tile_dim_apply(cbg_tile& t, int dim, const double* vec_host, int op, hipStream_t s);
+void restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile& out,
+                      hipStream_t s);
+
 }  // namespace cbg

@@ -406,6 +406,71 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
   return CBG_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// SpParMat::Transpose (SpParMat.cpp:3528-3590) on a square grid: a diagonal
+// rank transposes its tile; rank (r,c) transposes the tile of its complement
+// (c,r) (GetComplementRank), received over RCCL send/recv (host transport:
+// world broadcasts, test only).  `out` is this rank's tile of the transpose.
+// ---------------------------------------------------------------------------
+int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
+  if (g->pr != g->pc) return CBG_ERR_NOTSQUARE;
+  hipStream_t cs = g->compute;
+  // essentials of every rank's tile (world allgather: collective, diagonal ranks too)
+  int64_t e[4] = {T.m, T.n, T.nnz, T.nzc};
+  std::vector<int64_t> E((size_t)4 * g->nranks);
+  allgather_i64(g, COMM_WORLD, e, E.data(), 4);
+  const bool diag = g->prow == g->pcol;
+  const int peer = g->pcol * g->pc + g->prow;
+  const int64_t* pe = &E[4 * (size_t)peer];
+  cbg_tile R{};
+  if (!diag) tile_alloc_device(R, pe[0], pe[1], pe[2], pe[3]);
+  if (g->host_mode && g->nranks > 1) {
+    // every off-diagonal rank broadcasts its tile over the world communicator
+    for (int q = 0; q < g->nranks; ++q) {
+      const int qr = q / g->pc, qc = q % g->pc;
+      if (qr == qc) continue;
+      const int64_t* qe = &E[4 * (size_t)q];
+      const bool mine = q == g->rank, keep = !diag && q == peer;
+      auto hb = [&](void* dst, const void* src, size_t bytes) {
+        if (bytes == 0) return;
+        std::vector<char> h(bytes);
+        if (mine) CBG_HIP(hipMemcpy(h.data(), src, bytes, hipMemcpyDeviceToHost));
+        host_check(g->hc.bcast(g->hc.user, COMM_WORLD, h.data(), bytes, q), "transpose bcast");
+        if (keep) CBG_HIP(hipMemcpy(dst, h.data(), bytes, hipMemcpyHostToDevice));
+      };
+      hb(R.cp, T.cp, sizeof(int64_t) * (qe[3] + 1));
+      hb(R.jc, T.jc, sizeof(int32_t) * qe[3]);
+      hb(R.ir, T.ir, sizeof(int32_t) * qe[2]);
+      hb(R.val, T.val, sizeof(double) * qe[2]);
+    }
+  } else if (!diag) {
+    ncclComm_t c = g->world;
+    CBG_NCCL(ncclGroupStart());
+    CBG_NCCL(ncclSend(T.cp, T.nzc + 1, ncclInt64, peer, c, g->comm));
+    CBG_NCCL(ncclRecv(R.cp, pe[3] + 1, ncclInt64, peer, c, g->comm));
+    if (T.nzc) CBG_NCCL(ncclSend(T.jc, T.nzc, ncclInt32, peer, c, g->comm));
+    if (pe[3]) CBG_NCCL(ncclRecv(R.jc, pe[3], ncclInt32, peer, c, g->comm));
+    if (T.nnz) {
+      CBG_NCCL(ncclSend(T.ir, T.nnz, ncclInt32, peer, c, g->comm));
+      CBG_NCCL(ncclSend(T.val, T.nnz, ncclFloat64, peer, c, g->comm));
+    }
+    if (pe[2]) {
+      CBG_NCCL(ncclRecv(R.ir, pe[2], ncclInt32, peer, c, g->comm));
+      CBG_NCCL(ncclRecv(R.val, pe[2], ncclFloat64, peer, c, g->comm));
+    }
+    CBG_NCCL(ncclGroupEnd());
+    CBG_HIP(hipStreamSynchronize(g->comm));
+  }
+  if (diag) {
+    tile_transpose(T, out, cs);
+  } else {
+    tile_transpose(R, out, cs);
+    tile_free_device(R);
+  }
+  return CBG_OK;
+}
+
 }  // namespace cbg
 
 extern "C" int cbg_get_unique_id(void* id) {

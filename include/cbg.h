@@ -97,6 +97,21 @@ int cbg_tile_digest(const cbg_tile* t, int64_t row_off, int64_t col_off, uint64_
  * Device tiles; *equal receives 1 or 0. */
 int cbg_tile_equal(const cbg_tile* a, const cbg_tile* b, double epsilon, int* equal);
 
+/* ---------------- Galerkin triple-product path (GalerkinNew.cpp:96-153) ---------------- */
+/* SpDCCols::Transpose (SpDCCols.cpp:853-873): out = t^T as a device DCSC tile */
+int cbg_tile_transpose(const cbg_tile* t, cbg_tile* out);
+/* SpParMat::DimApply (SpParMat.cpp:801): dim CBG_DIM_COLUMN: x(i,j) = op(x(i,j), vec[j]);
+ * CBG_DIM_ROW: x(i,j) = op(x(i,j), vec[i]); vec is HOST memory of t->n (t->m) values,
+ * the tile's slice of the distributed dense vector.  In place. */
+enum { CBG_DIM_COLUMN = 0, CBG_DIM_ROW = 1 };
+enum { CBG_OP_MULTIPLIES = 0, CBG_OP_PLUS = 1, CBG_OP_MIN = 2, CBG_OP_MAX = 3 };
+int cbg_tile_dim_apply(cbg_tile* t, int dim, const double* vec, int op);
+/* Restriction operator of the Galerkin driver (mfiles/genrestrict.m: n x n/order,
+ * about n nonzeros, values in (0,1]): T(i, c(i)) = v(i) for every fine row i with
+ * c(i), v(i) from a counter-based hash of (seed, i), so every grid shape sees the
+ * same global T.  Tile (prow,pcol) of the pr x pc block distribution. */
+int cbg_restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile* out);
+
 /* ---------------- generator ---------------- */
 /* Graph500 Kronecker R-MAT as DistEdgeList::GenGraph500Data(packed, scrambled)
  * (DistEdgeList.cpp:223-280, RefGen21.h:73-318) -> SpParMat(DEL,false)
@@ -171,6 +186,12 @@ typedef int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg
 int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
                             int64_t B_gnrow, int semiring, int algo, int exec, int phases, cbg_phase_fn fn,
                             void* user, cbg_tile* C_local);
+
+/* SpParMat::Transpose (SpParMat.cpp:3528-3590), collective over a square grid:
+ * out = this rank's tile of the transposed matrix (the transpose of the
+ * complement rank's tile, exchanged with RCCL send/recv).  CBG_ERR_NOTSQUARE
+ * on non-square grids, like the reference. */
+int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out);
 
 #ifdef __cplusplus
 }

@@ -194,3 +194,54 @@ def abs_tile(t):
     u = dict(t)
     u["val"] = np.abs(t["val"])
     return u
+
+
+# ---- Galerkin path host restatements (checkers) ----
+_M64 = (1 << 64) - 1
+
+
+def _mix_np(z):
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def restriction_host(scale, order=2, seed=0x5EED):
+    """global restriction operator of cbg_restriction_tile (csrc/cbg_ops.hip k_restrict_keys)."""
+    n = 1 << scale
+    nc = n // order
+    i = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = _mix_np(np.uint64(seed) ^ (i * np.uint64(0xD1B54A32D192ED03)))
+    c = (h % np.uint64(nc)).astype(np.int64)
+    v = ((_mix_np(h) >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    order_ = np.lexsort((np.arange(n), c))
+    rows, cols, vals = np.arange(n)[order_], c[order_], v[order_]
+    jc, start = np.unique(cols, return_index=True)
+    return dict(m=n, n=nc, cp=np.append(start, n).astype(np.int64), jc=jc.astype(np.int32),
+                ir=rows.astype(np.int32), val=vals)
+
+
+def transpose_host(d):
+    cols = np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"]))
+    rows = d["ir"].astype(np.int64)
+    o = np.lexsort((cols, rows))
+    r, c, v = rows[o], cols[o], d["val"][o]
+    jc, start = np.unique(r, return_index=True)
+    return dict(m=d["n"], n=d["m"], cp=np.append(start, len(r)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=c.astype(np.int32), val=v)
+
+
+def add_diag_host(d, dv):
+    """d + diag(dv) for a host DCSC dict with no diagonal entries (loops removed)."""
+    n = len(dv)
+    cols = np.concatenate([np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"])), np.arange(n)])
+    rows = np.concatenate([d["ir"].astype(np.int64), np.arange(n)])
+    vals = np.concatenate([d["val"], dv])
+    o = np.lexsort((rows, cols))
+    r, c, v = rows[o], cols[o], vals[o]
+    jc, start = np.unique(c, return_index=True)
+    return dict(m=d["m"], n=d["n"], cp=np.append(start, len(r)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=r.astype(np.int32), val=v)

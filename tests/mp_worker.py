@@ -60,6 +60,41 @@ def main():
         if rank == 0:
             print("MPOK" if ok else "MULTTEST FAILED", flush=True)
         return
+    if case == "galerkin":
+        # GalerkinNew on a square grid: distributed Transpose (complement-rank
+        # exchange), PSpGEMMs, DimApply, +=, operator==; SAT digest vs the oracle
+        from helpers import add_diag_host, oracle_local, restriction_host, transpose_host
+        import pickle
+        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        scale, n = 10, 1 << 10
+        dv = np.random.default_rng(7).uniform(0.5, 1.5, n)
+        Lh = load_npz("rmat_s10_ef16_A.npz")
+        Ah = add_diag_host(Lh, dv)
+        L = cbg.SpParMat.from_global(grid, Lh)
+        A = cbg.SpParMat.from_global(grid, Ah)
+        T = cbg.SpParMat.restriction(grid, scale, 2)
+        S = T.copy()
+        S.Transpose()
+        SAT = cbg.PSpGEMM(S, cbg.PSpGEMM(A, T))
+        SLT = cbg.PSpGEMM(S, cbg.PSpGEMM(L, T))
+        SD = S.copy()
+        SD.DimApply(cbg.Column, dv)
+        SLT += cbg.PSpGEMM(SD, T)
+        ok = SLT == SAT
+        r0, _ = cbg.block_range(SAT.gm, pr, grid.prow)
+        c0, _ = cbg.block_range(SAT.gn, pc, grid.pcol)
+        d = SAT.tile.digest(r0, c0)
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(d))))]
+        tot = add_digests(alld)
+        Th = restriction_host(scale, 2)
+        ref = digest(oracle_local(transpose_host(Th), oracle_local(Ah, Th)))
+        ok = ok and tot["nnz"] == ref["nnz"] and tot["hs"] == ref["hs"]
+        ok = ok and abs(tot["vsum"] - ref["vsum"]) < 1e-9 * abs(ref["vsum"])
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if ok else f"GALERKIN FAILED {tot} vs {ref}", flush=True)
+        return
     if case.startswith("rmat"):
         A = load_npz("rmat_s10_ef16_A.npz")
         B = A

@@ -16,11 +16,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """a port p with p and p+1 (the TCP host-transport hub) free, drawn below the
+    Linux ephemeral range so that outgoing connections cannot take it meanwhile"""
+    import random
+    rng = random.Random(os.getpid() ^ int.from_bytes(os.urandom(4), "little"))
+    for _ in range(200):
+        p = rng.randrange(20000, 32000, 2)
+        try:
+            for q in (p, p + 1):
+                s = socket.socket()
+                s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                s.bind(("127.0.0.1", q))
+                s.close()
+            return p
+        except OSError:
+            continue
+    raise RuntimeError("no free port pair")
 
 
 def launch(nproc, args, timeout=300):
@@ -53,4 +64,12 @@ def test_summa_multiprocess_gpu(grid, case):
 def test_multtest_multiprocess_gpu(grid):
     """MultTest's SpGEMM checks (ParallelReadMM + operator== against CControl) on a grid."""
     rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "multtest"], timeout=600)
+    assert rc == 0 and "MPOK" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(2, 2)])
+def test_galerkin_multiprocess_gpu(grid):
+    """GalerkinNew on a 2x2 grid: distributed Transpose + PSpGEMM + DimApply + += (host transport)."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "galerkin"], timeout=600)
     assert rc == 0 and "MPOK" in out, out[-3000:]
