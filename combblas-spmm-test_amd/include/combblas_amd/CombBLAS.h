@@ -11,6 +11,9 @@
 //   Mult_AnXBn_Synch           ParFriends.h:1004  Mult_AnXBn_Synch
 //   PSpGEMM                    SpParMat.h:454     PSpGEMM
 //   MemEfficientSpGEMM         ParFriends.h:449   MemEfficientSpGEMM (phases; no MCL pruning)
+//   SpParMat::Transpose        SpParMat.cpp:3528  Transpose (square grids, RCCL send/recv)
+//   SpParMat::DimApply         SpParMat.cpp:801   DimApply (dense vector given as its global values)
+//   SpParMat::operator+=       SpParMat.cpp:741   operator+= (device merge)
 //   SpDCCols/SpParMat ==       SpDCCols.h:74, SpParMat.cpp:2878  operator== (ErrorTolerantEqual)
 //
 // Same template parameters and call shapes, so MultTiming/MultTest-style
@@ -50,6 +53,11 @@ inline void cbg_abort_on(int rc, const char* what) {
 }
 
 // ---------------------------------------------------------------- semirings
+enum Dim { Column = 0, Row = 1 };  // SpDefs.h
+// functors usable with DimApply (std::multiplies<double> etc. of the reference)
+template <class T> struct multiplies { static const int code = CBG_OP_MULTIPLIES; T operator()(T a, T b) const { return a * b; } };
+template <class T> struct plus { static const int code = CBG_OP_PLUS; T operator()(T a, T b) const { return a + b; } };
+
 // Operations.h maximum<T> (the BinOp MultTest passes to ParallelReadMM)
 template <class T>
 struct maximum {
@@ -297,6 +305,42 @@ class SpParMat {
   }
   DER& seq() const { return *spSeq; }
   std::shared_ptr<CommGrid> getcommgrid() const { return commGrid; }
+  // SpParMat::Transpose (SpParMat.cpp:3528-3590): in place, square grids
+  void Transpose() {
+    cbg_tile t{};
+    cbg_abort_on(cbg_grid_transpose(commGrid->handle(), spSeq->tile(), &t), "Transpose");
+    spSeq->reset(t);
+    std::swap(m_, n_);
+  }
+  // SpParMat::DimApply (SpParMat.cpp:801) with the distributed vector's global
+  // values (FullyDistVec is not on this path); op: a functor class below
+  template <typename Op>
+  void DimApply(Dim dim, const std::vector<double>& global, Op) {
+    const int parts = dim == Column ? commGrid->GetGridCols() : commGrid->GetGridRows();
+    const int idx = dim == Column ? commGrid->GetRankInProcRow() : commGrid->GetRankInProcCol();
+    const int64_t total = dim == Column ? (int64_t)n_ : (int64_t)m_;
+    const int64_t per = total / parts, lo = idx * per;
+    cbg_abort_on(cbg_tile_dim_apply(spSeq->tile(), dim == Column ? CBG_DIM_COLUMN : CBG_DIM_ROW, global.data() + lo,
+                                    Op::code),
+                 "DimApply");
+  }
+  // SpParMat::operator+= (SpParMat.cpp:741): union with duplicates added
+  SpParMat& operator+=(const SpParMat& rhs) {
+    cbg_tile parts[2] = {*spSeq->tile(), *rhs.spSeq->tile()}, c{};
+    cbg_abort_on(cbg_merge(parts, 2, CBG_PLUS_TIMES, &c, nullptr), "operator+=");
+    spSeq->reset(c);
+    return *this;
+  }
+  // restriction operator (mfiles/genrestrict.m role): n x n/order
+  static SpParMat restriction(std::shared_ptr<CommGrid> g, int scale, int order, uint64_t seed = 0x5EED) {
+    cbg_tile t{};
+    cbg_abort_on(cbg_restriction_tile(scale, order, seed, g->GetGridRows(), g->GetGridCols(), g->GetRankInProcCol(),
+                                      g->GetRankInProcRow(), &t),
+                 "restriction");
+    const IT n = (IT)1 << scale;
+    return SpParMat(new DER(t), g, n, n / order);
+  }
+
   // SpParMat::operator== (SpParMat.cpp:2878-2884): local equality, AND over the grid
   bool operator==(const SpParMat& rhs) const {
     int64_t bad = (*spSeq == *rhs.spSeq) ? 0 : 1;

@@ -400,3 +400,16 @@ def test_galerkin_driver():
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["splitting_correct"] and out["full_restriction_s"] > 0 and out["full_restriction_minplus_s"] > 0
+
+
+def test_cpp_galerkin_driver():
+    """tools/galerkin (C++ mirror: Transpose, DimApply, +=, PSpGEMM, operator==) on one rank."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "tools", "galerkin")
+    if not os.path.exists(exe):
+        pytest.skip("tools/galerkin not built (needs MPICH in /opt/conda)")
+    r = subprocess.run([exe, "12", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Splitting approach is correct" in r.stdout
