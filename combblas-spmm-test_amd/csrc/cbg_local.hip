@@ -292,51 +292,108 @@ constexpr int BIG_BS = 512;
 constexpr int SPARSE_SLAB_MAX = 4096;   // products of a (column, panel) pair counted by hash -> hash slab
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 
-// cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r
+// cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r.
+// A panel without rows of A(:,k) gets {q, q} with q the lower bound of the
+// panel's first row, so that {cmapP[r0].x, cmapP[r1].y} is A(:,k)'s run over
+// the panels r0..r1 (panel groups).  Columns absent from A stay {0, 0}.
 __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
-                                const int32_t* __restrict__ irA, int plog, int64_t nA1, int2* __restrict__ cmapP) {
+                                const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
+                                int2* __restrict__ cmapP) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t i = t / FLOP_G;  // FLOP_G lanes per A column
   if (i >= nzcA) return;
   const int64_t k = jcA[i], a = cpA[i], e = cpA[i + 1];
   for (int64_t q = a + t % FLOP_G; q < e; q += FLOP_G) {
     const int pnl = irA[q] >> plog;
-    if (q == a || (irA[q - 1] >> plog) != pnl) cmapP[pnl * nA1 + k].x = (int)q;
-    if (q == e - 1 || (irA[q + 1] >> plog) != pnl) cmapP[pnl * nA1 + k].y = (int)(q + 1);
+    const int prev = q == a ? -1 : irA[q - 1] >> plog;
+    const int next = q == e - 1 ? R : irA[q + 1] >> plog;
+    if (prev != pnl) {
+      for (int p = prev + 1; p < pnl; ++p) cmapP[p * nA1 + k] = make_int2((int)q, (int)q);
+      cmapP[pnl * nA1 + k].x = (int)q;
+    }
+    if (next != pnl) {
+      cmapP[pnl * nA1 + k].y = (int)(q + 1);
+      if (q == e - 1)
+        for (int p = pnl + 1; p < R; ++p) cmapP[p * nA1 + k] = make_int2((int)e, (int)e);
+    }
   }
 }
 
-// symbolic of one (big column, panel): bitmap of the panel's rows, per fine
-// range counts, slab plan; optionally keeps the bitmap for the numeric phase
-__global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict__ perm_big, int R,
-                                                      const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                      const int2* __restrict__ cmapP, int64_t nA1,
-                                                      const int32_t* __restrict__ irA, int64_t m, int plog,
-                                                      int32_t* __restrict__ cnt, int32_t* __restrict__ cnt_br,
-                                                      int4* __restrict__ desc, int32_t* __restrict__ nslab,
-                                                      unsigned* __restrict__ gbm, int gbm_slots,
-                                                      int* __restrict__ gbm_next, int* __restrict__ gbm_slot,
-                                                      int gbm_min) {
+// symbolic of the big columns, one block per (column, panel group).
+//
+// A pair (column, panel) is counted into a bitmap of the panel's rows with
+// per fine range counts and a slab plan (the bitmap optionally kept for the
+// numeric phase); a pair with few products is counted with an LDS hash sized
+// to it and becomes ONE sparse (hash) slab, so that its cost scales with its
+// products, not with the panel's 2^plog rows.
+//
+// Panel groups: a column with few products per panel (R-MAT rows are
+// scrambled, so a column's products spread evenly over the panels) is taken
+// 2^glog panels at a time -- the launch class fixes glog from the column's
+// flops -- and a group whose nonzeros fit one hash slab becomes ONE sparse
+// slab over the group's rows.  That shares the B column staging and column
+// map hops of up to 16 panels and reads A's runs over the group contiguously.
+constexpr int GROUP_LOG_MAX = 4;      // groups of up to 16 panels
+constexpr int GROUP_PRODUCTS = 2048;  // expected products of a group (launch class thresholds; 1024/3072/4096 measured slower)
+constexpr int GROUP_T = 16384;        // LDS hash of a group's symbolic (ints): products <= 8192
+constexpr int SPARSE_NNZ_MAX = 4096;  // nonzeros of a hash slab (largest numeric table: 8192)
+
+struct SymPanelArgs {
+  const int32_t* perm_big;
+  int R, plog, glog, boff, hwords;
+  const int64_t* cpB;
+  const int32_t* irB;
+  const int2* cmapP;
+  int64_t nA1;
+  const int32_t* irA;
+  int64_t m;
+  int32_t* cnt;
+  int32_t* cnt_br;
+  int4* desc;
+  int32_t* nslab;
+  unsigned* gbm;
+  int gbm_slots;
+  int* gbm_next;
+  int* gbm_slot;
+  int gbm_min;
+};
+
+struct SymPanelLds {
+  unsigned* bm;  // [hwords]: panel bitmap or hash keys
+  int* fine;     // [NFINE_MAX]
+  int* pref;     // [BIG_BS + 4]
+  int* st;       // [BIG_BS]
+  int* tmp;      // scan scratch
+};
+
+// one (column, panel) pair
+__device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLds& L, int b, int col, int r) {
   constexpr int BS = BIG_BS;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int R = a.R, plog = a.plog;
+  const int64_t* __restrict__ cpB = a.cpB;
+  const int32_t* __restrict__ irB = a.irB;
+  const int32_t* __restrict__ irA = a.irA;
+  int32_t* __restrict__ cnt = a.cnt;
+  int32_t* __restrict__ cnt_br = a.cnt_br;
+  int4* __restrict__ desc = a.desc;
+  int32_t* __restrict__ nslab = a.nslab;
+  unsigned* __restrict__ gbm = a.gbm;
+  const int gbm_slots = a.gbm_slots, gbm_min = a.gbm_min;
+  int* __restrict__ gbm_next = a.gbm_next;
+  int* __restrict__ gbm_slot = a.gbm_slot;
   const int pwords = 1 << (plog - 5);
   const int nfine = 1 << (plog - FINE_LOG);
-  unsigned* bm = reinterpret_cast<unsigned*>(smem);
-  int* fine = reinterpret_cast<int*>(bm + pwords);
-  int* pref = fine + NFINE_MAX;
-  int* st = pref + BS + 4;
-  int* tmp = st + BS;
+  unsigned* bm = L.bm;
+  int* fine = L.fine;
+  int* pref = L.pref;
+  int* st = L.st;
+  int* tmp = L.tmp;
   const int tid = threadIdx.x;
-  // panel-major block order: the blocks in flight gather A's panel-r segments
-  // (~1/R of A), which then stay in L2 / Infinity Cache
-  const int nbig = (int)(gridDim.x / R);
-  const int r = blockIdx.x / nbig, b = blockIdx.x % nbig;
-  const int br = b * R + r;
-  const int col = perm_big[b];
+  const int64_t br = (int64_t)b * R + r;
   const int R0 = r << plog;
-  const int R1 = (int)min((int64_t)R0 + (1LL << plog), m);
+  const int R1 = (int)min((int64_t)R0 + (1LL << plog), a.m);
   const int words = (R1 - R0 + 31) >> 5;
-  const int2* cm = cmapP + (int64_t)r * nA1;
+  const int2* cm = a.cmapP + (int64_t)r * a.nA1;
   unsigned long long tmark = wall_clock64();
   const int64_t p0 = cpB[col], p1 = cpB[col + 1];
   int64_t prod = 0;  // products of the pair
@@ -499,6 +556,101 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(const int32_t* __restrict_
   if (c_dbg & 16) {
     __syncthreads();
     phase_mark(tmark, 12);
+  }
+}
+
+// a panel group (column, panels r0..r1) counted as ONE hash slab over its
+// rows when its products fit the LDS hash and its nonzeros one hash slab;
+// false: nothing was written and the caller runs the panels one by one
+__device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelLds& L, int b, int col, int r0,
+                                          int r1) {
+  constexpr int BS = BIG_BS;
+  const int tid = threadIdx.x;
+  const int64_t p0 = a.cpB[col], p1 = a.cpB[col + 1];
+  if (p1 - p0 > BS) return false;
+  const int2* c0 = a.cmapP + (int64_t)r0 * a.nA1;
+  const int2* c1 = a.cmapP + (int64_t)r1 * a.nA1;
+  const int64_t p = p0 + tid;
+  int s = 0, len = 0;
+  if (p < p1) {
+    const int k = a.irB[p];
+    s = c0[k].x;
+    len = c1[k].y - s;
+  }
+  int total;
+  const int ex = block_excl_scan<BS>(len, L.tmp, &total);
+  L.pref[tid] = ex;
+  if (tid == BS - 1) L.pref[BS] = total;
+  L.st[tid] = s;
+  int T = 512;
+  while (T < 2 * total) T <<= 1;
+  if (T > a.hwords) {
+    __syncthreads();
+    return false;
+  }
+  int* keys = reinterpret_cast<int*>(L.bm);
+  for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
+  if (tid == 0) L.fine[0] = 0;
+  __syncthreads();
+  int count = 0;
+  const int32_t* __restrict__ irA = a.irA;
+  const int* pref = L.pref;
+  const int* st = L.st;
+  block_products<BS>(
+      pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+      [&](const SegI& g, int u) { return irA[g.off + u]; },
+      [&](int row) {
+        unsigned h = ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1);
+        while (true) {
+          const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+          if (old == EMPTY_KEY) { ++count; break; }
+          if (old == row) break;
+          h = (h + 1) & (unsigned)(T - 1);
+        }
+      });
+  count = wave_sum(count);
+  if (lane_id() == 0 && count) atomicAdd(&L.fine[0], count);
+  __syncthreads();
+  const int cg = L.fine[0];
+  __syncthreads();
+  if (cg > SPARSE_NNZ_MAX) return false;
+  if (tid <= r1 - r0) {
+    const int64_t br = (int64_t)b * a.R + r0 + tid;
+    const bool first = tid == 0;
+    a.nslab[br] = (first && cg) ? 1 : 0;
+    a.cnt_br[br] = first ? cg : 0;
+    if (a.gbm_slot) a.gbm_slot[br] = -1;
+    if (first && cg)
+      a.desc[br * NFINE_MAX] =
+          make_int4(r0 << a.plog, (int)min((int64_t)(r1 + 1) << a.plog, a.m), 0, cg | SLAB_SPARSE);
+  }
+  if (tid == 0 && cg) atomicAdd(&a.cnt[col], cg);
+  return true;
+}
+
+// grid: RG groups x (columns of the class), group-major, so that the blocks in
+// flight gather A's segments of the same panels, which then stay in L2 /
+// Infinity Cache
+__global__ __launch_bounds__(BIG_BS) void k_sym_panel(SymPanelArgs a) {
+  constexpr int BS = BIG_BS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  SymPanelLds L;
+  L.bm = reinterpret_cast<unsigned*>(smem);
+  L.fine = reinterpret_cast<int*>(L.bm + a.hwords);
+  L.pref = L.fine + NFINE_MAX;
+  L.st = L.pref + BS + 4;
+  L.tmp = L.st + BS;
+  const int g = 1 << a.glog;
+  const int RG = (a.R + g - 1) >> a.glog;
+  const int ncls = (int)(gridDim.x / RG);
+  const int rg = blockIdx.x / ncls, bl = blockIdx.x % ncls;
+  const int b = a.boff + bl;
+  const int col = a.perm_big[b];
+  const int r0 = rg << a.glog, r1 = min(r0 + g, a.R) - 1;
+  if (r1 > r0 && sym_group(a, L, b, col, r0, r1)) return;
+  for (int r = r0; r <= r1; ++r) {
+    sym_pair(a, L, b, col, r);
+    if (r < r1) __syncthreads();  // LDS is reused by the next panel
   }
 }
 
@@ -771,9 +923,23 @@ struct SlabLds {
 constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
-template <int SR, int BS>
+// A's (row, value) of product position q: two SoA loads, or one 16-byte load
+// of the interleaved copy (AOS: {row, -, value}) -- one cache line request per
+// product instead of two where A's runs are short
+template <int SR, bool AOS>
+__device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                           const int4* __restrict__ aosA, int q, double b, int lo) {
+  if (AOS) {
+    const int4 e = aosA[q];
+    return RowVal{e.x - lo, Sem<SR>::mul(__hiloint2double(e.w, e.z), b)};
+  }
+  return RowVal{irA[q] - lo, Sem<SR>::mul(valA[q], b)};
+}
+
+template <int SR, int BS, bool AOS>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
                                               const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                              const int4* __restrict__ aosA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
   if (pass == 0) {
     block_products<BS>(
@@ -784,7 +950,7 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
     // ranks of a group of products are looked up before any accumulates
     block_products3<BS>(
         pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-        [&](const SegV& g, int u) { return RowVal{irA[g.off + u] - lo, Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const SegV& g, int u) { return a_rowval<SR, AOS>(irA, valA, aosA, g.off + u, g.b, lo); },
         [&](const RowVal& x) {
           const int w = x.row >> 5;
           return RowVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.v};
@@ -793,12 +959,13 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
   }
 }
 
-template <int SR, int CAP, int BS>
+template <int SR, int CAP, int BS, bool AOS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                  int64_t nA1, const int32_t* __restrict__ irA,
-                                                 const double* __restrict__ valA, int32_t* __restrict__ out_ir,
+                                                 const double* __restrict__ valA, const int4* __restrict__ aosA,
+                                                 int32_t* __restrict__ out_ir,
                                                  double* __restrict__ out_val, const unsigned* __restrict__ gbm) {
   // Persistent blocks (one per CU at this LDS size) pull slabs from a queue.
   // With one block per CU nothing else hides a slab's dependent global reads,
@@ -956,7 +1123,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         } else {
           total = pref[BS];
         }
-        if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, AOS>(pass, total, pref, st, bv, irA, valA, aosA, lo, bm, wpre, vals);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
       }
@@ -1000,12 +1167,13 @@ struct SlabHashLds {
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
-template <int SR, int LOGT, int BS, bool CMLEN>
+template <int SR, int LOGT, int BS, bool CMLEN, bool AOS>
 __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                       int64_t nA1, const int32_t* __restrict__ irA,
-                                                      const double* __restrict__ valA, int32_t* __restrict__ out_ir,
+                                                      const double* __restrict__ valA, const int4* __restrict__ aosA,
+                                                      int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
   // persistent blocks over a queue of hash slabs; the next slab's record and
   // B staging (irB/valB, then the A column map hop) are prefetched into
@@ -1044,28 +1212,33 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       p_bv1 = valB[r.p0 + BS + tid];
     }
   };
+  // A(:,k)'s run over the slab's rows: one map entry, or the first and last
+  // panels' entries of a panel group (rows [lo, hi) span panels r .. r1)
+  auto seg_of = [&](const SlabRec& r, int k) -> int2 {
+    const int2 e = cmapP[(int64_t)r.r * nA1 + k];
+    if (CMLEN) return make_int2(e.x, e.x + e.y);
+    const int r1 = (r.hi - 1) >> plog;
+    if (r1 == r.r) return e;
+    return make_int2(e.x, cmapP[(int64_t)r1 * nA1 + k].y);
+  };
   auto fetch2 = [&](const SlabRec& r) {
     if (!staged(r)) return;
-    const int2* cmr = cmapP + (int64_t)r.r * nA1;
-    if (tid < r.nb) p_ce0 = cmr[p_ir0];
-    if (PF > 1 && BS + tid < r.nb) p_ce1 = cmr[p_ir1];
-    if (CMLEN) {
-      p_ce0.y += p_ce0.x;
-      p_ce1.y += p_ce1.x;
-    }
+    if (tid < r.nb) p_ce0 = seg_of(r, p_ir0);
+    if (PF > 1 && BS + tid < r.nb) p_ce1 = seg_of(r, p_ir1);
   };
   SlabRec rec = list[i];
   fetch1(rec);
   fetch2(rec);
   while (true) {
     if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
-    const int2* cm = cmapP + (int64_t)rec.r * nA1;
     const bool pre = staged(rec);
+    unsigned long long tmark = wall_clock64();
     for (int j = tid; j < T; j += BS) {
       keys[j] = EMPTY_KEY;
       vals[j] = Sem<SR>::identity();
     }
     __syncthreads();
+    phase_mark(tmark, 7);
     const int inext = tmp[NW + 2];
     const bool has_next = inext < n;
     SlabRec nrec;
@@ -1082,8 +1255,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
           ce = c == 0 ? p_ce0 : p_ce1;
           bval = c == 0 ? p_bv0 : p_bv1;
         } else {
-          ce = cm[irB[p]];
-          if (CMLEN) ce.y += ce.x;
+          ce = seg_of(rec, irB[p]);
           bval = valB[p];
         }
         s = ce.x;
@@ -1096,17 +1268,23 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       st[tid] = s;
       bv[tid] = bval;
       __syncthreads();
+      phase_mark(tmark, 13);
       if (c == nch - 1 && has_next) fetch1(nrec);
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-          [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+          [&](const SegV& g, int u) { return a_rowval<SR, AOS>(irA, valA, aosA, g.off + u, g.b, 0); },
           [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
       __syncthreads();
+      phase_mark(tmark, 14);
     }
     if (has_next) fetch2(nrec);
-    const int bshift = plog > LOGNB ? plog - LOGNB : 0;
+    int sl = plog;  // emit buckets span 2^sl rows from lo (a panel group spans several panels)
+    if (!CMLEN)
+      while ((1LL << sl) < (int64_t)(rec.hi - rec.lo)) ++sl;
+    const int bshift = sl > LOGNB ? sl - LOGNB : 0;
     hash_emit_sorted<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val, rec.obase);
     __syncthreads();  // LDS is reset for the next slab
+    phase_mark(tmark, 15);
     if (!has_next) break;
     i = inext;
     rec = nrec;
@@ -1231,15 +1409,16 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
   rec[i] = r;
 }
 
-template <int LOGT, int BS, int SR>
+template <int LOGT, int BS, int SR, bool AOS = false>
 static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
                                   const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s,
-                                  DeferredFree& df) {
+                                  DeferredFree& df, const int4* aos) {
   if (n <= 0) return;
+  if (!AOS && aos) return launch_num_block_hash<LOGT, BS, SR, true>(perm, n, B, cmap, A, colptr, C, s, df, aos);
   DBuf<SlabRec> rec(n);
   hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
   constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS, true>;
+  auto k = k_num_slab_hash<SR, LOGT, BS, true, AOS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1252,7 +1431,7 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
-                     A.ir, A.val, C.ir, C.val);
+                     A.ir, A.val, aos, C.ir, C.val);
   df.take(rec);
   df.take(queue);
 }
@@ -1265,15 +1444,17 @@ struct BigPlan {
   DBuf<int32_t> nslab, cnt_br;
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
+  const int4* aos = nullptr;  // interleaved (row, -, value) copy of A (numeric product loads), or none
 };
 
 
-template <int SR, int LOGT, int BS>
+template <int SR, int LOGT, int BS, bool AOS = false>
 static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                              cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
+  if (!AOS && bp.aos) return launch_slab_hash<SR, LOGT, BS, true>(list, n, bp, A, B, C, s, df);
   constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS, false>;
+  auto k = k_num_slab_hash<SR, LOGT, BS, false, AOS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1284,16 +1465,17 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
-                     A.n + 1, A.ir, A.val, C.ir, C.val);
+                     A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val);
   df.take(queue);
 }
 
-template <int SR, int CAP, int BS>
+template <int SR, int CAP, int BS, bool AOS = false>
 static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                                cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
+  if (!AOS && bp.aos) return launch_slab_bitmap<SR, CAP, BS, true>(list, n, bp, A, B, C, s, df);
   constexpr int L = SlabLds<CAP, BS>::BYTES;
-  auto k = k_num_slab<SR, CAP, BS>;
+  auto k = k_num_slab<SR, CAP, BS, AOS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1304,7 +1486,7 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
-                     A.n + 1, A.ir, A.val, C.ir, C.val, bp.gbm.p);
+                     A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val, bp.gbm.p);
   df.take(queue);
 }
 
@@ -1340,6 +1522,20 @@ static double bitmap_budget_bytes() {
   return (e ? atof(e) : 16.0) * 1e9;
 }
 
+static bool aos_enabled() {
+  static const char* e = getenv("CBG_AOS");  // measured: no gain at scale 22, -3 % at 18
+  return e && !strcmp(e, "1");
+}
+
+__global__ void k_aos(int64_t nnz, const int32_t* __restrict__ ir, const double* __restrict__ val,
+                      int4* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < nnz) {
+    const double v = val[i];
+    out[i] = make_int4(ir[i], 0, __double2loint(v), __double2hiint(v));
+  }
+}
+
 struct Binned {
   std::vector<int> count, offset;
   DBuf<int32_t> perm;
@@ -1349,7 +1545,7 @@ static void bin_columns(int64_t n, const int64_t* flops, const int32_t* cnt, int
                         int64_t big, Binned& out, hipStream_t s) {
   BinThr bt;
   bt.nb = nthr + 1;
-  for (int i = 0; i < nthr; ++i) bt.t[i] = (mode == 0) ? std::min(thr[i], big) : thr[i];
+  for (int i = 0; i < nthr; ++i) bt.t[i] = thr[i];
   DBuf<uint8_t> bin(n);
   DBuf<int> hist(2 * MAXBINS);
   CBG_HIP(hipMemsetAsync(hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
@@ -1386,7 +1582,8 @@ static bool block_bins_persistent() {
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
+                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df,
+                             const int4* aos) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
   launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, s);
@@ -1394,10 +1591,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
   if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df, aos);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df, aos);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df, aos);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df, aos);
   } else {
     launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
     launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
@@ -1461,6 +1658,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<int2> cmap(A.n + 1);
   CBG_HIP(hipMemsetAsync(cmap.p, 0, sizeof(int2) * (A.n + 1), s));
   hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
+  // interleaved copy of A for the numeric product loads (CBG_AOS=0 disables)
+  DBuf<int4> aos;
+  if (aos_enabled()) {
+    aos.reset(A.nnz);
+    hipLaunchKernelGGL(k_aos, dim3(nblk(A.nnz, 256)), dim3(256), 0, s, A.nnz, A.ir, A.val, aos.p);
+  }
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
   hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p);
@@ -1473,7 +1676,26 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
   }
-  bin_columns(nz, flops.p, cnt.p, 0, kSymThr, 7, big, sb, s);
+  // symbolic bins: kSymThr (clipped at `big`), then the big columns by panel
+  // group size 2^GROUP_LOG_MAX .. 1 (columns with F * g / R <= GROUP_PRODUCTS
+  // expected products per group; CBG_GROUPS=0 keeps every pair on its own)
+  BigPlan bp;
+  bp.plog = pick_panel_log(A.m);
+  bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
+  constexpr int NSMALL = 7, NGCLS = GROUP_LOG_MAX + 1;
+  {
+    static const char* eg = getenv("CBG_GROUPS");
+    static const char* ep = getenv("CBG_GROUP_PRODUCTS");
+    const bool groups = !(eg && !strcmp(eg, "0"));
+    const int64_t gp = ep ? atoll(ep) : GROUP_PRODUCTS;
+    int64_t thr[NSMALL + NGCLS - 1];
+    for (int i = 0; i < NSMALL; ++i) thr[i] = std::min(kSymThr[i], big);
+    for (int c = 0; c + 1 < NGCLS; ++c) {
+      const int64_t g = 1LL << (GROUP_LOG_MAX - c);
+      thr[NSMALL + c] = (groups && g <= bp.R) ? gp * bp.R / g : -1;
+    }
+    bin_columns(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sb, s);
+  }
   // small-column symbolic bins on the side stream, big columns on the main one
   fork(s);
   {
@@ -1486,11 +1708,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, side);
     launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, side);
   }
-  BigPlan bp;
-  bp.nbig = sb.count[7];
-  bp.perm_big = sb.perm.p + sb.offset[7];
-  bp.plog = pick_panel_log(A.m);
-  bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
+  bp.aos = aos.p;
+  bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
+  bp.perm_big = sb.perm.p + sb.offset[NSMALL];
   const int nbig = bp.nbig;
   const int64_t nbr = (int64_t)nbig * bp.R;
   if (nbig > 0) {
@@ -1501,7 +1721,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     } else {
       CBG_HIP(hipMemsetAsync(bp.cmapP.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
       hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * FLOP_G, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
-                         bp.plog, A.n + 1, bp.cmapP.p);
+                         bp.plog, bp.R, A.n + 1, bp.cmapP.p);
     }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
     bp.nslab.reset(nbr);
@@ -1518,13 +1738,25 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       gbm_next.reset(1);
       CBG_HIP(hipMemsetAsync(gbm_next.p, 0, sizeof(int), s));
     }
-    const size_t lds = (size_t)(1 << (bp.plog - 5)) * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 +
-                       (BIG_BS / WAVE + 4) * 4;
-    set_lds(k_sym_panel, lds);
     if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
-    hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)nbr), dim3(BIG_BS), lds, s, bp.perm_big, bp.R, B.cp, B.ir,
-                       bp.cmapP.p, A.n + 1, A.ir, A.m, bp.plog, cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p,
-                       (int)nslots, gbm_next.p, bp.gbm_slot.p, gbm_min_products());
+    const int pwords = 1 << (bp.plog - 5);
+    auto lds_of = [&](int hw) {
+      return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4;
+    };
+    set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
+    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, B.cp, B.ir, bp.cmapP.p, A.n + 1, A.ir, A.m,
+                    cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
+                    bp.gbm_slot.p, gbm_min_products()};
+    // one launch per group class (largest groups first)
+    for (int c = 0; c < NGCLS; ++c) {
+      const int nc = sb.count[NSMALL + c];
+      if (nc == 0) continue;
+      sa.glog = GROUP_LOG_MAX - c;
+      sa.boff = sb.offset[NSMALL + c] - sb.offset[NSMALL];
+      sa.hwords = sa.glog > 0 ? std::max(pwords, GROUP_T) : pwords;
+      const int64_t RG = (bp.R + (1 << sa.glog) - 1) >> sa.glog;
+      hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)(RG * nc)), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+    }
   }
   join(s);
   // column pointers of C
@@ -1572,8 +1804,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df);
-  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df);
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df, bp.aos);
+  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df, bp.aos);
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, df);
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, df);
@@ -1605,6 +1837,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
         if (k != 2) std::fprintf(stderr, " %s=%.3fms", names[k], ph[k] / 100.0 / 256.0 / 1000.0);
       const char* snames[5] = {"sym_staging", "sym_hash", "sym_bitmap_products", "sym_counts_store", "sym_plan"};
       for (int k = 8; k < 13; ++k) std::fprintf(stderr, " %s=%.3fms", snames[k - 8], ph[k] / 100.0 / 256.0 / 1000.0);
+      const char* hnames[4] = {"hash_clear", "hash_staging", "hash_products", "hash_emit"};
+      const int hk[4] = {7, 13, 14, 15};
+      for (int k = 0; k < 4; ++k) std::fprintf(stderr, " %s=%.3fms", hnames[k], ph[hk[k]] / 100.0 / 256.0 / 1000.0);
       std::fprintf(stderr, "\n");
       std::memset(ph, 0, sizeof(ph));
       CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph)));

@@ -114,6 +114,85 @@ def test_big_columns_tall_matrix(cbg):
     assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh))
 
 
+def _panel_group_operands():
+    """Tall A (m = 2^20 + 77: 5 row panels of 2^18, the last one partial) and a B whose
+    columns land in every big-column class: panel groups of 4 and 2 (expected products
+    per group <= 4096), single-panel hash pairs, bitmap pairs, a group with > 512 B
+    entries, and groups whose products crowd into one panel (nnz > one hash slab), which
+    must fall back to per-panel slabs."""
+    rng = np.random.default_rng(11)
+    m = (1 << 20) + 77
+    heavy, light, local = 3000, 1000, 200  # A columns: 100 rows anywhere / 8 rows / 100 rows in panel 0
+
+    def col(nr, hi):
+        return np.sort(rng.choice(hi, nr, replace=False))
+
+    acols = [col(100, m) for _ in range(heavy)] + [col(8, m) for _ in range(light)] + \
+            [col(100, 1 << 18) for _ in range(local)]
+    k = len(acols)
+    cnt = np.array([len(c) for c in acols])
+    Ah = dict(m=m, n=k, cp=np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64), jc=np.arange(k, dtype=np.int32),
+              ir=np.concatenate(acols).astype(np.int32),
+              val=rng.integers(1, 5, int(cnt.sum())).astype(np.float64))
+    groups = [(100, 5, 40, 0), (100, 44, 48, 0), (100, 78, 84, 0), (50, 140, 160, 0), (30, 280, 320, 0),
+              (20, 600, 601, 1), (20, 45, 46, 2)]
+    bcols = []
+    for num, lo, hi, kind in groups:
+        for _ in range(num):
+            nb = int(rng.integers(lo, hi))
+            if kind == 0:
+                bcols.append(np.sort(rng.choice(heavy, nb, replace=False)))
+            elif kind == 1:
+                bcols.append(np.sort(heavy + rng.choice(light, nb, replace=False)))
+            else:
+                bcols.append(np.sort(heavy + light + rng.choice(local, nb, replace=False)))
+    n = len(bcols)
+    perm = rng.permutation(n)
+    bcols = [bcols[i] for i in perm]
+    bc = np.array([len(c) for c in bcols])
+    Bh = dict(m=k, n=n, cp=np.concatenate([[0], np.cumsum(bc)]).astype(np.int64), jc=np.arange(n, dtype=np.int32),
+              ir=np.concatenate(bcols).astype(np.int32), val=rng.integers(1, 3, int(bc.sum())).astype(np.float64))
+    return Ah, Bh
+
+
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_panel_groups_tall_matrix(cbg, sr):
+    """Big columns in panel groups (one hash slab over several row panels), their
+    per-panel fallbacks and a partial last panel, bit-exact against the oracle."""
+    Ah, Bh = _panel_group_operands()
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr)
+    assert cbg.last_stats()["n_big"] > 300
+    assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh, sr))
+
+
+def test_panel_groups_rmat20():
+    """R-MAT scale 20 (4 row panels): the panel-group path and the per-pair path
+    (CBG_GROUPS=0) give identical C (digest), and nnz(C) equals the reference's
+    symbolic total (golden)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, json
+sys.path.insert(0, "tests")
+from conftest import load_cbg
+cbg = load_cbg()
+A = cbg.rmat_tile(20, 16); B = cbg.rmat_tile(20, 16)
+print(json.dumps(cbg.LocalHybridSpGEMM(A, B).digest()))
+'''
+    res = []
+    for env in ({}, {"CBG_GROUPS": "0"}):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **env),
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    g = G["rmat"]["s20_ef16"]["symbolic"]
+    assert res[0]["nnz"] == g["nnzC"]
+    assert res[0] == res[1]
+
+
 def test_edge_cases(cbg):
     # empty operands -> SpTuples(0, m, n) (mtSpGEMM.h:224-227)
     E = dict(m=5, n=4, cp=np.zeros(1, np.int64), jc=np.zeros(0, np.int32), ir=np.zeros(0, np.int32),
