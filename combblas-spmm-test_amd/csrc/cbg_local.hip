@@ -334,7 +334,7 @@ __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, c
 // slab over the group's rows.  That shares the B column staging and column
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
 constexpr int GROUP_LOG_MAX = 4;      // groups of up to 16 panels
-constexpr int GROUP_PRODUCTS = 2048;  // expected products of a group (launch class thresholds; 1024/3072/4096 measured slower)
+constexpr int GROUP_PRODUCTS = 3072;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
 constexpr int GROUP_T = 16384;        // LDS hash of a group's symbolic (ints): products <= 8192
 constexpr int SPARSE_NNZ_MAX = 4096;  // nonzeros of a hash slab (largest numeric table: 8192)
 
@@ -667,6 +667,10 @@ struct __attribute__((aligned(16))) SlabRec {
   int pad;
 };
 
+#ifndef CBG_HASH_LOAD_NUM  // numeric hash slab tables: T >= (NUM/DEN) * nnz
+#define CBG_HASH_LOAD_NUM 3  // 3/2: +4.6 % at scale 22 over 2/1 (more hash slabs in the smaller, higher-occupancy classes)
+#define CBG_HASH_LOAD_DEN 2
+#endif
 // slab work lists per launch class.  Classes: 0 bitmap small (nnz <=
 // small_cap), 1 bitmap large, 2+k hash slab with table 2^(SLAB_HASH_LOG0+k).
 constexpr int SLAB_HASH_LOG0 = 9, SLAB_HASH_NCLS = 5;  // tables 512 .. 8192
@@ -675,7 +679,7 @@ __device__ __forceinline__ int slab_class(int w, int small_cap) {
   if (w & SLAB_SPARSE) {
     const int c = w & (SLAB_SPARSE - 1);
     int k = 0;
-    while ((1 << (SLAB_HASH_LOG0 + k)) < 2 * c) ++k;
+    while ((1 << (SLAB_HASH_LOG0 + k)) * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // table load <= NUM/DEN
     return 2 + k;
   }
   return w <= small_cap ? 0 : 1;
@@ -1160,9 +1164,10 @@ template <int LOGT, int BS>
 struct SlabHashLds {
   static constexpr int T = 1 << LOGT;
   static constexpr int NB = T / 4;  // row buckets of the sorted emit
-  // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[T/2] u16
+  static constexpr int MEMB = (T * CBG_HASH_LOAD_DEN + CBG_HASH_LOAD_NUM - 1) / CBG_HASH_LOAD_NUM;  // max nnz
+  // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
-                               (2 * NB + 4) * 4 + (T / 2) * 2;
+                               (2 * NB + 4) * 4 + MEMB * 2;
 };
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
@@ -1517,9 +1522,19 @@ static int gbm_min_products() {
   return e ? atoi(e) : 0;
 }
 
+// kept symbolic bitmaps (32 KiB per (column, panel) pair): CBG_BITMAP_BUDGET_GB,
+// default 48 GB (scale 22 on one GPU: 16 GB -> 32 GB was +3.7 %), never more
+// than a quarter of the device memory still available (free + pool cache), so
+// that C, allocated after the symbolic phase, keeps room
 static double bitmap_budget_bytes() {
   static const char* e = getenv("CBG_BITMAP_BUDGET_GB");
-  return (e ? atof(e) : 16.0) * 1e9;
+  const double want = (e ? atof(e) : 48.0) * 1e9;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return std::min(want, 16e9);
+  }
+  return std::min(want, 0.25 * (double)(fr + pool().bytes_cached()));
 }
 
 static bool aos_enabled() {
