@@ -335,7 +335,14 @@ __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, c
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
 constexpr int GROUP_LOG_MAX = 4;      // groups of up to 16 panels
 constexpr int GROUP_PRODUCTS = 3072;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
-constexpr int GROUP_T = 16384;        // LDS hash of a group's symbolic (ints): products <= 8192
+#ifndef CBG_GROUP_T
+#define CBG_GROUP_T 8192  // = the panel bitmap words: group launches keep 4 blocks/CU (+1 % at scale 22 over 16384 at load 1/2)
+#endif
+#ifndef CBG_SYM_LOAD_NUM  // symbolic group hash: T >= (NUM/DEN) * products
+#define CBG_SYM_LOAD_NUM 3
+#define CBG_SYM_LOAD_DEN 2
+#endif
+constexpr int GROUP_T = CBG_GROUP_T;  // LDS hash of a group's symbolic (ints)
 constexpr int SPARSE_NNZ_MAX = 4096;  // nonzeros of a hash slab (largest numeric table: 8192)
 
 struct SymPanelArgs {
@@ -583,7 +590,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   if (tid == BS - 1) L.pref[BS] = total;
   L.st[tid] = s;
   int T = 512;
-  while (T < 2 * total) T <<= 1;
+  while (T * CBG_SYM_LOAD_DEN < CBG_SYM_LOAD_NUM * total) T <<= 1;
   if (T > a.hwords) {
     __syncthreads();
     return false;
