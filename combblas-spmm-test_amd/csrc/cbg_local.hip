@@ -140,6 +140,24 @@ __device__ __forceinline__ void hash_acc(int* keys, double* vals, int row, doubl
   }
 }
 
+// the same for a table of any size T (multiplicative hash scaled to [0, T))
+template <int T>
+__device__ __forceinline__ unsigned hash_slot_t(int key) {
+  return (unsigned)(((unsigned long long)((unsigned)key * 0x9E3779B1u) * T) >> 32);
+}
+template <int SR, int T>
+__device__ __forceinline__ void hash_acc_t(int* keys, double* vals, int row, double v) {
+  unsigned h = hash_slot_t<T>(row);
+  while (true) {
+    const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+    if (old == EMPTY_KEY || old == row) {
+      Sem<SR>::lds_acc(&vals[h], v);
+      return;
+    }
+    h = h + 1 == T ? 0u : h + 1;
+  }
+}
+
 // ----------------------------------------------------------------------------
 // symbolic: wave per column, LDS hash of row ids
 // ----------------------------------------------------------------------------
@@ -679,14 +697,18 @@ struct __attribute__((aligned(16))) SlabRec {
 #define CBG_HASH_LOAD_DEN 2
 #endif
 // slab work lists per launch class.  Classes: 0 bitmap small (nnz <=
-// small_cap), 1 bitmap large, 2+k hash slab with table 2^(SLAB_HASH_LOG0+k).
-constexpr int SLAB_HASH_LOG0 = 9, SLAB_HASH_NCLS = 5;  // tables 512 .. 8192
+// small_cap), 1 bitmap large, 2+k hash slab with table HASH_T[k] slots: powers
+// of two and 1.5x powers of two, so that the LDS a slab reserves (12 B per
+// slot) tracks its nnz and more slabs fit a CU
+constexpr int SLAB_HASH_NCLS = 9;
+#define CBG_HASH_TABLES 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192
+__constant__ int c_hash_t[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
 constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS;
 __device__ __forceinline__ int slab_class(int w, int small_cap) {
   if (w & SLAB_SPARSE) {
     const int c = w & (SLAB_SPARSE - 1);
     int k = 0;
-    while ((1 << (SLAB_HASH_LOG0 + k)) * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // table load <= NUM/DEN
+    while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
     return 2 + k;
   }
   return w <= small_cap ? 0 : 1;
@@ -1167,10 +1189,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 // numeric of a sparse (column, panel) pair (hash-mode slab, <= SPARSE_SLAB_MAX
 // products): LDS hash sized to the pair's nnz, sorted emit by row buckets
-template <int LOGT, int BS>
+template <int T_, int BS>
 struct SlabHashLds {
-  static constexpr int T = 1 << LOGT;
-  static constexpr int NB = T / 4;  // row buckets of the sorted emit
+  static constexpr int T = T_;
+  static constexpr int LOGNB = 31 - __builtin_clz(T / 4);
+  static constexpr int NB = 1 << LOGNB;  // row buckets of the sorted emit (power of two <= T/4)
   static constexpr int MEMB = (T * CBG_HASH_LOAD_DEN + CBG_HASH_LOAD_NUM - 1) / CBG_HASH_LOAD_NUM;  // max nnz
   // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
@@ -1179,7 +1202,7 @@ struct SlabHashLds {
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
-template <int SR, int LOGT, int BS, bool CMLEN, bool AOS>
+template <int SR, int TT, int BS, bool CMLEN, bool AOS>
 __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
@@ -1190,9 +1213,9 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   // persistent blocks over a queue of hash slabs; the next slab's record and
   // B staging (irB/valB, then the A column map hop) are prefetched into
   // registers while the current slab multiplies and emits (see k_num_slab)
-  using L = SlabHashLds<LOGT, BS>;
+  using L = SlabHashLds<TT, BS>;
   constexpr int T = L::T, NB = L::NB;
-  constexpr int LOGNB = LOGT - 2;
+  constexpr int LOGNB = L::LOGNB;
   constexpr int NW = BS / WAVE;
   constexpr int PF = (BIG_BS + BS - 1) / BS;  // prefetched chunks (hash slabs have <= BIG_BS B entries)
   static_assert(PF <= 2, "prefetch chunks");
@@ -1285,7 +1308,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
           [&](const SegV& g, int u) { return a_rowval<SR, AOS>(irA, valA, aosA, g.off + u, g.b, 0); },
-          [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
+          [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
       phase_mark(tmark, 14);
     }
@@ -1429,8 +1452,8 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   if (!AOS && aos) return launch_num_block_hash<LOGT, BS, SR, true>(perm, n, B, cmap, A, colptr, C, s, df, aos);
   DBuf<SlabRec> rec(n);
   hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
-  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS, true, AOS>;
+  constexpr int L = SlabHashLds<1 << LOGT, BS>::BYTES;
+  auto k = k_num_slab_hash<SR, 1 << LOGT, BS, true, AOS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1460,13 +1483,13 @@ struct BigPlan {
 };
 
 
-template <int SR, int LOGT, int BS, bool AOS = false>
+template <int SR, int T, int BS, bool AOS = false>
 static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                              cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  if (!AOS && bp.aos) return launch_slab_hash<SR, LOGT, BS, true>(list, n, bp, A, B, C, s, df);
-  constexpr int L = SlabHashLds<LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, LOGT, BS, false, AOS>;
+  if (!AOS && bp.aos) return launch_slab_hash<SR, T, BS, true>(list, n, bp, A, B, C, s, df);
+  constexpr int L = SlabHashLds<T, BS>::BYTES;
+  auto k = k_num_slab_hash<SR, T, BS, false, AOS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1514,12 +1537,16 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   }
   launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s, df);
   launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s, df);
-  static_assert(SLAB_HASH_LOG0 == 9 && SLAB_HASH_NCLS == 5, "hash slab classes");
-  launch_slab_hash<SR, 9, 256>(at[2], ncls[2], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 10, 256>(at[3], ncls[3], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 11, 256>(at[4], ncls[4], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 12, 512>(at[5], ncls[5], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 13, 512>(at[6], ncls[6], bp, A, B, C, s, df);
+  static_assert(SLAB_HASH_NCLS == 9, "hash slab classes (CBG_HASH_TABLES)");
+  launch_slab_hash<SR, 512, 256>(at[2], ncls[2], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 768, 256>(at[3], ncls[3], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 1024, 256>(at[4], ncls[4], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 1536, 256>(at[5], ncls[5], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 2048, 256>(at[6], ncls[6], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 3072, 512>(at[7], ncls[7], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 4096, 512>(at[8], ncls[8], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, s, df);
 }
 
 // (column, panel) pairs with fewer products re-mark their bitmap in the numeric
@@ -1814,8 +1841,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipStreamSynchronize(s));
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
-      std::fprintf(stderr, "[cbg slabs] bitmap small %d large %d | hash T512 %d T1024 %d T2048 %d T4096 %d T8192 %d\n",
-                   ncls[0], ncls[1], ncls[2], ncls[3], ncls[4], ncls[5], ncls[6]);
+    {
+      static const int ht[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
+      std::fprintf(stderr, "[cbg slabs] bitmap small %d large %d | hash", ncls[0], ncls[1]);
+      for (int k = 0; k < SLAB_HASH_NCLS; ++k) std::fprintf(stderr, " T%d %d", ht[k], ncls[2 + k]);
+      std::fprintf(stderr, "\n");
+    }
   }
   // output arrays
   C.nnz = nnzc;
