@@ -528,14 +528,25 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     __syncthreads();
     if (tmp[0] >= 0) gdst = gbm + (int64_t)tmp[0] * pwords;
   }
-  for (int j = tid; j - lane_id() < words; j += BS) {
-    unsigned x = 0;
-    if (j < words) {
-      x = bm[j];
-      if (gdst) gdst[j] = x;
+  {
+    // wave w owns the fine ranges w, w + 8, ...: its lanes read (and store)
+    // 64 consecutive words per step, and one wave reduction per fine range
+    constexpr int FW = 1 << (FINE_LOG - 5);  // words per fine range
+    const int w = tid / WAVE, lane = lane_id();
+    for (int f = w; f * FW < words; f += BS / WAVE) {
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < FW; q += WAVE) {
+        const int j = f * FW + q + lane;
+        if (j < words) {
+          const unsigned x = bm[j];
+          if (gdst) gdst[j] = x;
+          c += __popc(x);
+        }
+      }
+      c = wave_sum(c);
+      if (lane == 0) fine[f] = c;
     }
-    const int c = wave_sum(__popc(x));
-    if (lane_id() == 0 && c) atomicAdd(&fine[j >> (FINE_LOG - 5)], c);
   }
   __syncthreads();
   phase_mark(tmark, 11);
