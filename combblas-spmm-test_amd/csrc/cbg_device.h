@@ -23,16 +23,27 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (WAVE - 1); }
 
-// inclusive scan over the 64 lanes of a wave
+// DPP lane move with zero fill: lanes whose source is outside the row (or in
+// a row masked off by ROWM) read 0
+template <int CTRL, int ROWM = 0xf>
+__device__ __forceinline__ int dpp0(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWM, 0xf, false);
+}
+
+// inclusive scan over the 64 lanes of a wave, on the VALU: row_shr 1/2/4/8
+// inside rows of 16 lanes, then row_bcast 15/31 across rows (no LDS
+// permutes, whose latency a __shfl_up ladder would pay six times)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < WAVE; d <<= 1) {
-    int t = __shfl_up(v, d, WAVE);
-    if (lane >= d) v += t;
-  }
+  v += dpp0<0x111>(v);       // row_shr:1
+  v += dpp0<0x112>(v);       // row_shr:2
+  v += dpp0<0x114>(v);       // row_shr:4
+  v += dpp0<0x118>(v);       // row_shr:8
+  v += dpp0<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp0<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
   return v;
 }
+// value of lane 63 in every lane
+__device__ __forceinline__ int wave_last(int v) { return __builtin_amdgcn_readlane(v, WAVE - 1); }
 __device__ __forceinline__ long long wave_incl_scan64(long long v) {
   const int lane = lane_id();
 #pragma unroll
@@ -47,11 +58,7 @@ __device__ __forceinline__ long long wave_sum64(long long v) {
   for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, WAVE);
   return v;
 }
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int d = WAVE / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, WAVE);
-  return v;
-}
+__device__ __forceinline__ int wave_sum(int v) { return wave_last(wave_incl_scan(v)); }
 
 // Block-wide exclusive scan of one int per thread.  `tmp` holds >= BS/64+1 ints.
 // Returns the exclusive prefix; *total receives the block sum.  Contains barriers.
@@ -109,7 +116,7 @@ __device__ __forceinline__ int block_ordered_scan(int n, G&& get, P&& put, int* 
     const int c = (i < b1) ? get(i) : 0;
     const int incl = wave_incl_scan(c);
     if (i < b1) put(i, run + incl - c);
-    run += __shfl(incl, WAVE - 1, WAVE);
+    run += wave_last(incl);
   }
   const int total = tmp[NW];
   __syncthreads();

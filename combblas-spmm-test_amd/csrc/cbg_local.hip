@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void k_sym_wave(const int32_t* __restrict__ pe
       len = e.y;
     }
     const int incl = wave_incl_scan(len);
-    const int total = __shfl(incl, WAVE - 1, WAVE);
+    const int total = wave_last(incl);
     pref[lane + 1] = incl;
     if (lane == 0) pref[0] = 0;
     st[lane] = s;
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
       bval = valB[p];
     }
     const int incl = wave_incl_scan(len);
-    const int total = __shfl(incl, WAVE - 1, WAVE);
+    const int total = wave_last(incl);
     pref[lane + 1] = incl;
     if (lane == 0) pref[0] = 0;
     st[lane] = s;
