@@ -133,6 +133,22 @@ __device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
   return lo;
 }
 
+// seg_search for the 64 consecutive products [u0, umax] of a wave (all lanes
+// active, nseg a multiple of 64): one sampled read per lane and two ballots
+// narrow every lane's search to the samples spanning [u0, umax], so a lane
+// pays ~log2(nseg/64) + 2 dependent LDS reads instead of log2(nseg)
+__device__ __forceinline__ int seg_search_wave(const int* pref, int nseg, int u, int u0, int umax) {
+  const int S = nseg / WAVE;
+  const int smp = pref[lane_id() * S];
+  const int c0 = __popcll(__ballot(smp <= u0)), c1 = __popcll(__ballot(smp <= umax));
+  int lo = (c0 - 1) * S, hi = c1 * S;  // pref[lo] <= u0 <= u <= umax < pref[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pref[mid] <= u) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 // Flattened product loop over a staged chunk of B entries.  pref[0..nseg] is
 // the prefix sum of the segment lengths (A sub-columns); product u belongs to
 // segment sg with pref[sg] <= u < pref[sg+1].  Lanes of a wave take
@@ -149,9 +165,11 @@ __device__ __forceinline__ int seg_search(const int* pref, int n, int u) {
 template <class S, class L, class P, class A>
 __device__ __forceinline__ void wave_products3(const int* pref, int nseg, int u0, int u1, S&& seg, L&& load, P&& pre,
                                                A&& apply) {
+  if (u0 >= u1) return;  // (uniform: the whole wave)
+  const int umax = min(u0 + WAVE - 1, u1 - 1);
   int u = u0 + lane_id();
+  int sg = seg_search_wave(pref, nseg, min(u, umax), u0, umax);
   if (u >= u1) return;
-  int sg = seg_search(pref, nseg, u);
   int nxt = pref[sg + 1];
   auto cur = seg(sg);
   auto advance = [&](int v) {
