@@ -62,27 +62,21 @@ __device__ __forceinline__ int wave_sum(int v) { return wave_last(wave_incl_scan
 
 // Block-wide exclusive scan of one int per thread.  `tmp` holds >= BS/64+1 ints.
 // Returns the exclusive prefix; *total receives the block sum.  Contains barriers.
+// The wave totals are combined by every wave on its own (one LDS read per
+// lane and a DPP scan), not by a serial loop of thread 0 behind a second barrier.
 template <int BS>
 __device__ __forceinline__ int block_excl_scan(int v, int* tmp, int* total) {
   constexpr int NW = BS / WAVE;
+  static_assert(NW <= WAVE, "block size");
   const int lane = lane_id(), w = threadIdx.x / WAVE;
-  int incl = wave_incl_scan(v);
+  const int incl = wave_incl_scan(v);
   if (lane == WAVE - 1) tmp[w] = incl;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int i = 0; i < NW; ++i) {
-      int t = tmp[i];
-      tmp[i] = s;
-      s += t;
-    }
-    tmp[NW] = s;
-  }
-  __syncthreads();
-  int r = tmp[w] + incl - v;
-  *total = tmp[NW];
-  __syncthreads();
-  return r;
+  const int ws = wave_incl_scan(lane < NW ? tmp[lane] : 0);
+  const int before = w > 0 ? __builtin_amdgcn_readlane(ws, w > 0 ? w - 1 : 0) : 0;
+  *total = __builtin_amdgcn_readlane(ws, NW - 1);
+  __syncthreads();  // tmp is reused by the caller
+  return before + incl - v;
 }
 
 // Block-wide exclusive scan of get(i), i in [0, n), in index order: put(i, prefix)
