@@ -95,24 +95,15 @@ __device__ __forceinline__ int block_ordered_scan(int n, G&& get, P&& put, int* 
   tot = wave_sum(tot);
   if (lane == 0) tmp[w] = tot;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int q = 0; q < NW; ++q) {
-      const int t = tmp[q];
-      tmp[q] = s;
-      s += t;
-    }
-    tmp[NW] = s;
-  }
-  __syncthreads();
-  int run = tmp[w];
+  const int ws = wave_incl_scan(lane < NW ? tmp[lane] : 0);  // every wave combines the wave totals itself
+  int run = w > 0 ? __builtin_amdgcn_readlane(ws, w > 0 ? w - 1 : 0) : 0;
+  const int total = __builtin_amdgcn_readlane(ws, NW - 1);
   for (int i = b0 + lane; i - lane < b1; i += WAVE) {
     const int c = (i < b1) ? get(i) : 0;
     const int incl = wave_incl_scan(c);
     if (i < b1) put(i, run + incl - c);
     run += wave_last(incl);
   }
-  const int total = tmp[NW];
   __syncthreads();
   return total;
 }
