@@ -102,6 +102,16 @@ struct LocalStats {
 void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s,
                   LocalStats* st = nullptr);
 LocalStats& thread_stats();
+// A-side preparation (column maps of A) kept across the local multiplies of
+// one MemEfficientSpGEMM call, whose phases all multiply the same A: between
+// aprep_begin() and aprep_end() on a thread, a local multiply whose A has the
+// same arrays and sizes as the previous one reuses its maps.
+void aprep_begin();
+void aprep_end();
+struct APrepScope {
+  APrepScope() { aprep_begin(); }
+  ~APrepScope() { aprep_end(); }
+};
 
 // device exclusive scan of n int64 values -> out[0..n], returns nothing (total at out[n])
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);

@@ -1485,7 +1485,8 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
 struct BigPlan {
   int nbig = 0, R = 1, plog = 0;
   const int32_t* perm_big = nullptr;
-  DBuf<int2> cmapP;
+  const int2* cmapP = nullptr;  // panel column maps (cached across phases, or cmapP_own)
+  DBuf<int2> cmapP_own;
   DBuf<int4> desc;
   DBuf<int32_t> nslab, cnt_br;
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
@@ -1510,7 +1511,7 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
   const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                      A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val);
   df.take(queue);
 }
@@ -1531,7 +1532,7 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP.p,
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                      A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val, bp.gbm.p);
   df.take(queue);
 }
@@ -1663,6 +1664,29 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   }
 }
 
+struct APrep {
+  bool active = false;
+  const void* ir = nullptr;
+  const void* cp = nullptr;
+  int64_t nnz = -1, nzc = -1, m = -1, n = -1;
+  DBuf<int2> cmap, cmapP;  // cmapP: built by the first call that had big columns
+  int plog = -1;
+};
+static APrep& aprep() {
+  static thread_local APrep a;
+  return a;
+}
+void aprep_begin() { aprep().active = true; }
+void aprep_end() {
+  APrep& a = aprep();
+  a.cmap.release();
+  a.cmapP.release();
+  a.active = false;
+  a.ir = a.cp = nullptr;
+  a.nnz = a.nzc = a.m = a.n = -1;
+  a.plog = -1;
+}
+
 LocalStats& thread_stats() {
   static thread_local LocalStats t;
   return t;
@@ -1714,10 +1738,28 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipEventCreate(&ev2));
   CBG_HIP(hipEventRecord(ev0, s));
   const int64_t nz = B.nzc;
-  // A column map
-  DBuf<int2> cmap(A.n + 1);
-  CBG_HIP(hipMemsetAsync(cmap.p, 0, sizeof(int2) * (A.n + 1), s));
-  hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
+  // A column map (reused across the phases of one MemEfficientSpGEMM)
+  APrep& ap = aprep();
+  const bool a_hit = ap.active && ap.ir == A.ir && ap.cp == A.cp && ap.nnz == A.nnz && ap.nzc == A.nzc &&
+                     ap.m == A.m && ap.n == A.n;
+  if (ap.active && !a_hit) {
+    ap.cmap.release();
+    ap.cmapP.release();
+    ap.ir = A.ir;
+    ap.cp = A.cp;
+    ap.nnz = A.nnz;
+    ap.nzc = A.nzc;
+    ap.m = A.m;
+    ap.n = A.n;
+    ap.plog = -1;
+  }
+  DBuf<int2> cmap_own;
+  DBuf<int2>& cmap = ap.active ? ap.cmap : cmap_own;
+  if (!a_hit) {
+    cmap.reset(A.n + 1);
+    CBG_HIP(hipMemsetAsync(cmap.p, 0, sizeof(int2) * (A.n + 1), s));
+    hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
+  }
   // interleaved copy of A for the numeric product loads (CBG_AOS=0 disables)
   DBuf<int4> aos;
   if (aos_enabled()) {
@@ -1774,14 +1816,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const int nbig = bp.nbig;
   const int64_t nbr = (int64_t)nbig * bp.R;
   if (nbig > 0) {
-    // panel column maps of A
-    bp.cmapP.reset((size_t)bp.R * (A.n + 1));
-    if (bp.R == 1) {
-      hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, bp.cmapP.p);
+    // panel column maps of A (reused across phases like cmap)
+    if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
+      bp.cmapP = ap.cmapP.p;
     } else {
-      CBG_HIP(hipMemsetAsync(bp.cmapP.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
-      hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * FLOP_G, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
-                         bp.plog, bp.R, A.n + 1, bp.cmapP.p);
+      DBuf<int2>& cp = ap.active ? ap.cmapP : bp.cmapP_own;
+      cp.reset((size_t)bp.R * (A.n + 1));
+      if (bp.R == 1) {
+        hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, cp.p);
+      } else {
+        CBG_HIP(hipMemsetAsync(cp.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
+        hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * FLOP_G, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc,
+                           A.ir, bp.plog, bp.R, A.n + 1, cp.p);
+      }
+      if (ap.active) ap.plog = bp.plog;
+      bp.cmapP = cp.p;
     }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
     bp.nslab.reset(nbr);
@@ -1804,7 +1853,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4;
     };
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
-    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, B.cp, B.ir, bp.cmapP.p, A.n + 1, A.ir, A.m,
+    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p, gbm_min_products()};
     // one launch per group class (largest groups first)

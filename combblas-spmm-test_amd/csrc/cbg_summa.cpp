@@ -377,6 +377,7 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
   for (int p = 0; p < phases; ++p) off[p] = (int64_t)p * w;
   std::vector<cbg_tile> parts;
   int cb_rc = 0;
+  APrepScope aprep_scope;  // every phase multiplies the same A
   for (int p = 0; p < phases; ++p) {
     cbg_tile Cp{};
     const int rc = summa_spgemm(g, A, pieces[p], A_gncol, B_gnrow, sr, algo, exec, Cp);
