@@ -55,8 +55,12 @@ __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int3
 // flops of every B column: FLOP_G lanes per column (B columns are short on
 // average; a whole wave per column would leave most lanes idle)
 constexpr int FLOP_G = 16;
+// flops[nzcB] accumulates the total (one atomic per block)
 __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
                         const int2* __restrict__ cmap, int64_t* __restrict__ flops) {
+  __shared__ unsigned long long bsum;
+  if (threadIdx.x == 0) bsum = 0;
+  __syncthreads();
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t w = t / FLOP_G;
   const int g = (int)(t % FLOP_G);
@@ -65,7 +69,12 @@ __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int
     for (int64_t p = cpB[w] + g; p < cpB[w + 1]; p += FLOP_G) s += cmap[irB[p]].y;
 #pragma unroll
   for (int d = FLOP_G / 2; d > 0; d >>= 1) s += __shfl_xor(s, d, FLOP_G);
-  if (w < nzcB && g == 0) flops[w] = s;
+  if (w < nzcB && g == 0) {
+    flops[w] = s;
+    atomicAdd(&bsum, (unsigned long long)s);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && bsum) atomicAdd(reinterpret_cast<unsigned long long*>(flops + nzcB), bsum);
 }
 
 // panel column map when A has a single row panel: {start, end} from cmap
@@ -1768,6 +1777,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
+  CBG_HIP(hipMemsetAsync(flops.p + nz, 0, sizeof(int64_t), s));
   hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p);
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
@@ -1967,11 +1977,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     st->nnz = nnzc;
     st->n_big = nbig;
     st->n_slabs = nslabs;
-    // total flops (reduction on host is fine: nz is small relative to the work)
-    std::vector<int64_t> f(nz);
-    CBG_HIP(hipMemcpy(f.data(), flops.p, sizeof(int64_t) * nz, hipMemcpyDeviceToHost));
-    int64_t tot = 0;
-    for (int64_t v : f) tot += v;
+    int64_t tot = 0;  // total flops (k_flops)
+    CBG_HIP(hipMemcpy(&tot, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost));
     st->flops = tot;
   }
   (void)hipEventDestroy(ev0);
