@@ -362,6 +362,9 @@ __global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, c
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
 constexpr int GROUP_LOG_MAX = 4;      // groups of up to 16 panels
 constexpr int GROUP_PRODUCTS = 3072;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
+#ifndef CBG_SYM_WAVES_OF_UNITS  // persistent symbolic grid: resident blocks x this
+#define CBG_SYM_WAVES_OF_UNITS 32  // 1: -2 % (static stride meets hub-column imbalance); 16-32: +1 % at scale 22
+#endif
 #ifndef CBG_GROUP_T
 #define CBG_GROUP_T 8192  // = the panel bitmap words: group launches keep 4 blocks/CU (+1 % at scale 22 over 16384 at load 1/2)
 #endif
@@ -375,6 +378,7 @@ constexpr int SPARSE_NNZ_MAX = 4096;  // nonzeros of a hash slab (largest numeri
 struct SymPanelArgs {
   const int32_t* perm_big;
   int R, plog, glog, boff, hwords;
+  int ncls;  // columns of this launch class (units = ncls x panel groups)
   const int64_t* cpB;
   const int32_t* irB;
   const int2* cmapP;
@@ -392,6 +396,17 @@ struct SymPanelArgs {
   int gbm_min;
 };
 
+// staging of a unit fetched ahead: ok = 1: p0/p1 of the column; ok = 2: also
+// this thread's first-chunk A run (s, len) over the unit's rows
+struct SymPre {
+  int64_t p0 = 0, p1 = 0;
+  int s = 0, len = 0;
+  int ok = 0;
+};
+struct NoHook {
+  __device__ void operator()(int) const {}
+};
+
 struct SymPanelLds {
   unsigned* bm;  // [hwords]: panel bitmap or hash keys
   int* fine;     // [NFINE_MAX]
@@ -401,7 +416,9 @@ struct SymPanelLds {
 };
 
 // one (column, panel) pair
-__device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLds& L, int b, int col, int r) {
+template <class H>
+__device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLds& L, int b, int col, int r,
+                                         const SymPre& pre, H& hook) {
   constexpr int BS = BIG_BS;
   const int R = a.R, plog = a.plog;
   const int64_t* __restrict__ cpB = a.cpB;
@@ -429,7 +446,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int words = (R1 - R0 + 31) >> 5;
   const int2* cm = a.cmapP + (int64_t)r * a.nA1;
   unsigned long long tmark = wall_clock64();
-  const int64_t p0 = cpB[col], p1 = cpB[col + 1];
+  const int64_t p0 = pre.ok ? pre.p0 : cpB[col], p1 = pre.ok ? pre.p1 : cpB[col + 1];
   int64_t prod = 0;  // products of the pair
   if (p1 - p0 <= BS) {
     // single chunk: stage once; a pair with few products is counted with an
@@ -437,7 +454,10 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     // scales with its products, not with the panel's 2^plog rows
     const int64_t p = p0 + tid;
     int s = 0, len = 0;
-    if (p < p1) {
+    if (pre.ok == 2) {
+      s = pre.s;
+      len = pre.len;
+    } else if (p < p1) {
       const int2 e = cm[irB[p]];
       s = e.x;
       len = e.y - e.x;
@@ -448,6 +468,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = s;
     prod = total;
+    hook(1);
     phase_mark(tmark, 8);
     int T = 512;
     while (T < 2 * total) T <<= 1;
@@ -468,6 +489,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
               h = (h + 1) & (unsigned)(T - 1);
             }
           });
+      hook(2);
       count = wave_sum(count);
       if (tid == 0) fine[0] = 0;
       __syncthreads();
@@ -510,6 +532,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     if (tid == BS - 1) pref[BS] = total;
     prod += total;
     st[tid] = s;
+    hook(1);
     __syncthreads();
     if (!(c_dbg & 1))
       block_products<BS>(
@@ -519,6 +542,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     __syncthreads();
   }
   }
+  hook(2);
   phase_mark(tmark, 10);
   // per fine range popcounts: coalesced words; a wave's 64 words lie in one
   // fine range (2^(FINE_LOG-5) >= 64 words)
@@ -607,17 +631,21 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
 // a panel group (column, panels r0..r1) counted as ONE hash slab over its
 // rows when its products fit the LDS hash and its nonzeros one hash slab;
 // false: nothing was written and the caller runs the panels one by one
+template <class H>
 __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelLds& L, int b, int col, int r0,
-                                          int r1) {
+                                          int r1, const SymPre& pre, H& hook) {
   constexpr int BS = BIG_BS;
   const int tid = threadIdx.x;
-  const int64_t p0 = a.cpB[col], p1 = a.cpB[col + 1];
+  const int64_t p0 = pre.ok ? pre.p0 : a.cpB[col], p1 = pre.ok ? pre.p1 : a.cpB[col + 1];
   if (p1 - p0 > BS) return false;
   const int2* c0 = a.cmapP + (int64_t)r0 * a.nA1;
   const int2* c1 = a.cmapP + (int64_t)r1 * a.nA1;
   const int64_t p = p0 + tid;
   int s = 0, len = 0;
-  if (p < p1) {
+  if (pre.ok == 2) {
+    s = pre.s;
+    len = pre.len;
+  } else if (p < p1) {
     const int k = a.irB[p];
     s = c0[k].x;
     len = c1[k].y - s;
@@ -627,6 +655,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   L.pref[tid] = ex;
   if (tid == BS - 1) L.pref[BS] = total;
   L.st[tid] = s;
+  hook(1);
   int T = 512;
   while (T * CBG_SYM_LOAD_DEN < CBG_SYM_LOAD_NUM * total) T <<= 1;
   if (T > a.hwords) {
@@ -653,6 +682,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
           h = (h + 1) & (unsigned)(T - 1);
         }
       });
+  hook(2);
   count = wave_sum(count);
   if (lane_id() == 0 && count) atomicAdd(&L.fine[0], count);
   __syncthreads();
@@ -677,6 +707,11 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
 // flight gather A's segments of the same panels, which then stay in L2 /
 // Infinity Cache
 __global__ __launch_bounds__(BIG_BS) void k_sym_panel(SymPanelArgs a) {
+  // Persistent blocks stride over the units (group-major order kept); the
+  // next unit's dependent loads -- column id, B column range, B rows, A run
+  // bounds -- are issued one per stage of the current unit (hook 1 after its
+  // staging, 2 after its products, 3 at its end) instead of back to back at
+  // the start of every block.
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   SymPanelLds L;
@@ -685,17 +720,71 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(SymPanelArgs a) {
   L.pref = L.fine + NFINE_MAX;
   L.st = L.pref + BS + 4;
   L.tmp = L.st + BS;
+  const int tid = threadIdx.x;
   const int g = 1 << a.glog;
   const int RG = (a.R + g - 1) >> a.glog;
-  const int ncls = (int)(gridDim.x / RG);
-  const int rg = blockIdx.x / ncls, bl = blockIdx.x % ncls;
-  const int b = a.boff + bl;
-  const int col = a.perm_big[b];
-  const int r0 = rg << a.glog, r1 = min(r0 + g, a.R) - 1;
-  if (r1 > r0 && sym_group(a, L, b, col, r0, r1)) return;
-  for (int r = r0; r <= r1; ++r) {
-    sym_pair(a, L, b, col, r);
-    if (r < r1) __syncthreads();  // LDS is reused by the next panel
+  const int ncls = a.ncls;
+  const int nunits = ncls * RG;
+  // next unit's fetch state
+  int n_b = 0, n_r0 = 0, n_r1 = 0, n_col = 0, n_k = -1, stage = -1;
+  int64_t n_p0 = 0, n_p1 = 0;
+  auto start = [&](int unit) {
+    stage = -1;
+    if (unit >= nunits) return;
+    const int rg = unit / ncls;
+    n_b = a.boff + unit % ncls;
+    n_r0 = rg << a.glog;
+    n_r1 = min(n_r0 + g, a.R) - 1;
+    n_col = a.perm_big[n_b];
+    stage = 0;
+  };
+  SymPre nxt;
+  auto hook = [&](int k) {
+    if (stage < 0) return;
+    if (k >= 1 && stage < 1) {
+      n_p0 = a.cpB[n_col];
+      n_p1 = a.cpB[n_col + 1];
+      stage = 1;
+    }
+    if (k >= 2 && stage < 2) {
+      n_k = (n_p1 - n_p0 <= BS && tid < n_p1 - n_p0) ? a.irB[n_p0 + tid] : -1;
+      stage = 2;
+    }
+    if (k >= 3 && stage < 3) {
+      nxt.p0 = n_p0;
+      nxt.p1 = n_p1;
+      nxt.s = nxt.len = 0;
+      nxt.ok = n_p1 - n_p0 <= BS ? 2 : 1;
+      if (n_k >= 0) {
+        const int2 e0 = a.cmapP[(int64_t)n_r0 * a.nA1 + n_k];
+        const int e1y = n_r1 > n_r0 ? a.cmapP[(int64_t)n_r1 * a.nA1 + n_k].y : e0.y;
+        nxt.s = e0.x;
+        nxt.len = e1y - e0.x;
+      }
+      stage = 3;
+    }
+  };
+  int unit = blockIdx.x;
+  start(unit);
+  hook(3);
+  while (unit < nunits) {
+    const SymPre cur = nxt;
+    const int b = n_b, col = n_col, r0 = n_r0, r1 = n_r1;
+    const int next = unit + (int)gridDim.x;
+    start(next);
+    bool done = false;
+    if (r1 > r0) done = sym_group(a, L, b, col, r0, r1, cur, hook);
+    if (!done) {
+      SymPre pp = cur;  // a group run by panels: the column range only
+      if (r1 > r0) pp.ok = pp.ok ? 1 : 0;
+      for (int r = r0; r <= r1; ++r) {
+        sym_pair(a, L, b, col, r, pp, hook);
+        if (r < r1) __syncthreads();  // LDS is reused by the next panel
+      }
+    }
+    hook(3);
+    __syncthreads();  // LDS is reused by the next unit
+    unit = next;
   }
 }
 
@@ -1863,7 +1952,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4;
     };
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
-    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
+    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p, gbm_min_products()};
     // one launch per group class (largest groups first)
@@ -1874,7 +1963,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       sa.boff = sb.offset[NSMALL + c] - sb.offset[NSMALL];
       sa.hwords = sa.glog > 0 ? std::max(pwords, GROUP_T) : pwords;
       const int64_t RG = (bp.R + (1 << sa.glog) - 1) >> sa.glog;
-      hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)(RG * nc)), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+      sa.ncls = nc;
+      static int per_cu = 0;  // resident blocks per CU at the largest LDS size
+      if (!per_cu) {
+        CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_sym_panel, BIG_BS,
+                                                             lds_of(std::max(pwords, GROUP_T))));
+        if (per_cu < 1) per_cu = 1;
+      }
+      const int64_t grid = std::min<int64_t>(RG * nc, (int64_t)per_cu * device_cus() * CBG_SYM_WAVES_OF_UNITS);
+      hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
     }
   }
   join(s);
