@@ -1653,8 +1653,12 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_hash<SR, 1024, 256>(at[4], ncls[4], bp, A, B, C, s, df);
   launch_slab_hash<SR, 1536, 256>(at[5], ncls[5], bp, A, B, C, s, df);
   launch_slab_hash<SR, 2048, 256>(at[6], ncls[6], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 3072, 512>(at[7], ncls[7], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 4096, 512>(at[8], ncls[8], bp, A, B, C, s, df);
+#ifndef CBG_HBS_3072
+#define CBG_HBS_3072 512
+#define CBG_HBS_4096 512
+#endif
+  launch_slab_hash<SR, 3072, CBG_HBS_3072>(at[7], ncls[7], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 4096, CBG_HBS_4096>(at[8], ncls[8], bp, A, B, C, s, df);
   launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, s, df);
   launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, s, df);
 }
