@@ -35,6 +35,8 @@ namespace cbg {
 __constant__ int c_dbg;
 //   16: k_num_slab accumulates per-phase wall time (thread 0 of every block) into g_phase
 __device__ unsigned long long g_phase[16];
+//   32: k_num_slab counts into g_stat: slabs, non-full slabs, B entries, B entries of non-full slabs, products, nout
+__device__ unsigned long long g_stat[8];
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
   if ((c_dbg & 16) && threadIdx.x == 0) {
     const unsigned long long n = wall_clock64();
@@ -1170,6 +1172,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int64_t obase = rec.obase;
     const bool have_bm = rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
     const bool pre = staged(rec);        // chunk 0 staging came in registers
+    if ((c_dbg & 32) && tid == 0) {
+      atomicAdd(&g_stat[0], 1ull);
+      atomicAdd(&g_stat[1], rec.full ? 0ull : 1ull);
+      atomicAdd(&g_stat[2], (unsigned long long)rec.nb);
+      atomicAdd(&g_stat[3], rec.full ? 0ull : (unsigned long long)rec.nb);
+      atomicAdd(&g_stat[5], (unsigned long long)rec.nout);
+      atomicAdd(&g_stat[6], rec.nb > BS ? 1ull : 0ull);
+    }
     unsigned long long tmark = wall_clock64();
 #pragma unroll
     for (int k = 0; k < WPT; ++k) {
@@ -2053,6 +2063,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   {
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16) {
+      if (dbg & 32) {
+        unsigned long long gs[8];
+        CBG_HIP(hipMemcpyFromSymbol(gs, HIP_SYMBOL(g_stat), sizeof(gs)));
+        std::fprintf(stderr, "[cbg k_num_slab] slabs %llu nonfull %llu nb %llu nb_nonfull %llu nout %llu multichunk %llu\n",
+                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6]);
+        std::memset(gs, 0, sizeof(gs));
+        CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stat), gs, sizeof(gs)));
+      }
       unsigned long long ph[16];
       CBG_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph)));
       const char* names[7] = {"init", "staging", "-", "rankscan", "pass0", "pass1", "output"};
