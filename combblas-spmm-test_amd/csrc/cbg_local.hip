@@ -317,7 +317,10 @@ constexpr int PANEL_LOG_MAX = CBG_PANEL_LOG_MAX;  // max rows of a panel (LDS bi
 static_assert(SLAB_CAP >= (1 << FINE_LOG), "a fine range must fit one slab");
 constexpr int SLAB_WORDS = 1 << (PANEL_LOG_MAX - 5);
 constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= max slabs) per panel
-constexpr int BIG_BS = 512;
+#ifndef CBG_BIG_BS
+#define CBG_BIG_BS 512
+#endif
+constexpr int BIG_BS = CBG_BIG_BS;
 constexpr int SPARSE_SLAB_MAX = 4096;   // products of a (column, panel) pair counted by hash -> hash slab
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 
@@ -1064,7 +1067,10 @@ struct SlabLds {
   static constexpr int BYTES = WPRE_OFF + SLAB_WORDS * 2;
   static_assert(BYTES <= 160 * 1024, "slab LDS");
 };
-constexpr int SLAB_SMALL_CAP = 2048, SLAB_SMALL_BS = 512;
+#ifndef CBG_SLAB_SMALL_CAP
+#define CBG_SLAB_SMALL_CAP 2048
+#endif
+constexpr int SLAB_SMALL_CAP = CBG_SLAB_SMALL_CAP, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
 // A's (row, value) of product position q: two SoA loads, or one 16-byte load
