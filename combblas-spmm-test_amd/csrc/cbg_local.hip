@@ -408,9 +408,6 @@ struct SymPre {
   int s = 0, len = 0;
   int ok = 0;
 };
-struct NoHook {
-  __device__ void operator()(int) const {}
-};
 
 struct SymPanelLds {
   unsigned* bm;  // [hwords]: panel bitmap or hash keys
@@ -1073,23 +1070,16 @@ struct SlabLds {
 constexpr int SLAB_SMALL_CAP = CBG_SLAB_SMALL_CAP, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
-// A's (row, value) of product position q: two SoA loads, or one 16-byte load
-// of the interleaved copy (AOS: {row, -, value}) -- one cache line request per
-// product instead of two where A's runs are short
-template <int SR, bool AOS>
-__device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const double* __restrict__ valA,
-                                           const int4* __restrict__ aosA, int q, double b, int lo) {
-  if (AOS) {
-    const int4 e = aosA[q];
-    return RowVal{e.x - lo, Sem<SR>::mul(__hiloint2double(e.w, e.z), b)};
-  }
+// A's (row, value) of product position q
+template <int SR>
+__device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const double* __restrict__ valA, int q,
+                                           double b, int lo) {
   return RowVal{irA[q] - lo, Sem<SR>::mul(valA[q], b)};
 }
 
-template <int SR, int BS, bool AOS>
+template <int SR, int BS>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
                                               const int32_t* __restrict__ irA, const double* __restrict__ valA,
-                                              const int4* __restrict__ aosA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
   if (pass == 0) {
     block_products<BS>(
@@ -1100,7 +1090,7 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
     // ranks of a group of products are looked up before any accumulates
     block_products3<BS>(
         pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-        [&](const SegV& g, int u) { return a_rowval<SR, AOS>(irA, valA, aosA, g.off + u, g.b, lo); },
+        [&](const SegV& g, int u) { return a_rowval<SR>(irA, valA, g.off + u, g.b, lo); },
         [&](const RowVal& x) {
           const int w = x.row >> 5;
           return RowVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.v};
@@ -1109,12 +1099,12 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
   }
 }
 
-template <int SR, int CAP, int BS, bool AOS>
+template <int SR, int CAP, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                  int64_t nA1, const int32_t* __restrict__ irA,
-                                                 const double* __restrict__ valA, const int4* __restrict__ aosA,
+                                                 const double* __restrict__ valA,
                                                  int32_t* __restrict__ out_ir,
                                                  double* __restrict__ out_val, const unsigned* __restrict__ gbm) {
   // Persistent blocks (one per CU at this LDS size) pull slabs from a queue.
@@ -1281,7 +1271,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         } else {
           total = pref[BS];
         }
-        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, AOS>(pass, total, pref, st, bv, irA, valA, aosA, lo, bm, wpre, vals);
+        if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
       }
@@ -1327,12 +1317,12 @@ struct SlabHashLds {
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
-template <int SR, int TT, int BS, bool CMLEN, bool AOS>
+template <int SR, int TT, int BS, bool CMLEN>
 __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                       int64_t nA1, const int32_t* __restrict__ irA,
-                                                      const double* __restrict__ valA, const int4* __restrict__ aosA,
+                                                      const double* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
   // persistent blocks over a queue of hash slabs; the next slab's record and
@@ -1432,7 +1422,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       if (c == nch - 1 && has_next) fetch1(nrec);
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-          [&](const SegV& g, int u) { return a_rowval<SR, AOS>(irA, valA, aosA, g.off + u, g.b, 0); },
+          [&](const SegV& g, int u) { return a_rowval<SR>(irA, valA, g.off + u, g.b, 0); },
           [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
       phase_mark(tmark, 14);
@@ -1569,16 +1559,15 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
   rec[i] = r;
 }
 
-template <int LOGT, int BS, int SR, bool AOS = false>
+template <int LOGT, int BS, int SR>
 static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
                                   const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s,
-                                  DeferredFree& df, const int4* aos) {
+                                  DeferredFree& df) {
   if (n <= 0) return;
-  if (!AOS && aos) return launch_num_block_hash<LOGT, BS, SR, true>(perm, n, B, cmap, A, colptr, C, s, df, aos);
   DBuf<SlabRec> rec(n);
   hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
   constexpr int L = SlabHashLds<1 << LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, 1 << LOGT, BS, true, AOS>;
+  auto k = k_num_slab_hash<SR, 1 << LOGT, BS, true>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1591,7 +1580,7 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
-                     A.ir, A.val, aos, C.ir, C.val);
+                     A.ir, A.val, C.ir, C.val);
   df.take(rec);
   df.take(queue);
 }
@@ -1605,17 +1594,15 @@ struct BigPlan {
   DBuf<int32_t> nslab, cnt_br;
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
-  const int4* aos = nullptr;  // interleaved (row, -, value) copy of A (numeric product loads), or none
 };
 
 
-template <int SR, int T, int BS, bool AOS = false>
+template <int SR, int T, int BS>
 static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                              cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  if (!AOS && bp.aos) return launch_slab_hash<SR, T, BS, true>(list, n, bp, A, B, C, s, df);
   constexpr int L = SlabHashLds<T, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, T, BS, false, AOS>;
+  auto k = k_num_slab_hash<SR, T, BS, false>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1626,17 +1613,16 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                     A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val);
+                     A.n + 1, A.ir, A.val, C.ir, C.val);
   df.take(queue);
 }
 
-template <int SR, int CAP, int BS, bool AOS = false>
+template <int SR, int CAP, int BS>
 static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
                                cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  if (!AOS && bp.aos) return launch_slab_bitmap<SR, CAP, BS, true>(list, n, bp, A, B, C, s, df);
   constexpr int L = SlabLds<CAP, BS>::BYTES;
-  auto k = k_num_slab<SR, CAP, BS, AOS>;
+  auto k = k_num_slab<SR, CAP, BS>;
   set_lds(k, L);
   static int per_cu = 0;
   if (!per_cu) {
@@ -1647,7 +1633,7 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                     A.n + 1, A.ir, A.val, bp.aos, C.ir, C.val, bp.gbm.p);
+                     A.n + 1, A.ir, A.val, C.ir, C.val, bp.gbm.p);
   df.take(queue);
 }
 
@@ -1701,20 +1687,6 @@ static double bitmap_budget_bytes() {
   return std::min(want, 0.25 * (double)(fr + pool().bytes_cached()));
 }
 
-static bool aos_enabled() {
-  static const char* e = getenv("CBG_AOS");  // measured: no gain at scale 22, -3 % at 18
-  return e && !strcmp(e, "1");
-}
-
-__global__ void k_aos(int64_t nnz, const int32_t* __restrict__ ir, const double* __restrict__ val,
-                      int4* __restrict__ out) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < nnz) {
-    const double v = val[i];
-    out[i] = make_int4(ir[i], 0, __double2loint(v), __double2hiint(v));
-  }
-}
-
 struct Binned {
   std::vector<int> count, offset;
   DBuf<int32_t> perm;
@@ -1761,8 +1733,7 @@ static bool block_bins_persistent() {
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df,
-                             const int4* aos) {
+                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
   launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, s);
@@ -1770,10 +1741,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
   if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df, aos);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df, aos);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df, aos);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df, aos);
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df);
   } else {
     launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
     launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
@@ -1878,12 +1849,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemsetAsync(cmap.p, 0, sizeof(int2) * (A.n + 1), s));
     hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
   }
-  // interleaved copy of A for the numeric product loads (CBG_AOS=0 disables)
-  DBuf<int4> aos;
-  if (aos_enabled()) {
-    aos.reset(A.nnz);
-    hipLaunchKernelGGL(k_aos, dim3(nblk(A.nnz, 256)), dim3(256), 0, s, A.nnz, A.ir, A.val, aos.p);
-  }
+
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
   CBG_HIP(hipMemsetAsync(flops.p + nz, 0, sizeof(int64_t), s));
@@ -1929,7 +1895,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, side);
     launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, side);
   }
-  bp.aos = aos.p;
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
   const int nbig = bp.nbig;
@@ -2044,8 +2009,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df, bp.aos);
-  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df, bp.aos);
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df);
+  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df);
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, df);
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, df);
