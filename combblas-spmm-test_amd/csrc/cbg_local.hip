@@ -1304,10 +1304,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 // numeric of a sparse (column, panel) pair (hash-mode slab, <= SPARSE_SLAB_MAX
 // products): LDS hash sized to the pair's nnz, sorted emit by row buckets
+#ifndef CBG_EMIT_NB_DIV  // emit buckets of a hash slab: power of two <= T / DIV
+#define CBG_EMIT_NB_DIV 4
+#endif
 template <int T_, int BS>
 struct SlabHashLds {
   static constexpr int T = T_;
-  static constexpr int LOGNB = 31 - __builtin_clz(T / 4);
+  static constexpr int LOGNB = 31 - __builtin_clz(T / CBG_EMIT_NB_DIV);
   static constexpr int NB = 1 << LOGNB;  // row buckets of the sorted emit (power of two <= T/4)
   static constexpr int MEMB = (T * CBG_HASH_LOAD_DEN + CBG_HASH_LOAD_NUM - 1) / CBG_HASH_LOAD_NUM;  // max nnz
   // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
