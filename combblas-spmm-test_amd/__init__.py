@@ -38,6 +38,7 @@ DOUBLEBUFF, SYNCH = 0, 1
 EXEC_PANEL, EXEC_STAGED = 0, 1
 
 GRIDMISMATCH, DIMMISMATCH, NOTSQUARE, MATRIXALIAS, INVALIDPARAMS = 3001, 3002, 3003, 3005, 3007
+NOTSUPPORTED = 3103
 
 
 class CbgError(RuntimeError):
@@ -69,7 +70,7 @@ EXPORTS = [
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
-    "cbg_grid_transpose",
+    "cbg_grid_transpose", "cbg_grid_block_extract",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -128,6 +129,7 @@ def lib():
         "cbg_tile_dim_apply": ([T, i32, ctypes.POINTER(ctypes.c_double), i32], i32),
         "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
         "cbg_grid_transpose": ([vp, T, T], i32),
+        "cbg_grid_block_extract": ([vp, T, i64, i64, i32, i64, i64, T], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -598,6 +600,31 @@ class SpParMat:
         self.tile.free()
         self.tile, self.gm, self.gn = t, self.gn, self.gm
 
+    def _block_extract(self, dim, lo, hi):
+        t = Tile()
+        _check(lib().cbg_grid_block_extract(self.grid.h, ctypes.byref(self.tile.c), self.gm, self.gn, dim, lo, hi,
+                                            ctypes.byref(t.c)))
+        return SpParMat(t, self.grid, hi - lo if dim == 0 else self.gm, hi - lo if dim == 1 else self.gn)
+
+    def BlockSplit(self, br, bc):
+        """SpParMat::BlockSplit (SpParMat.cpp:2974-3058): br x bc blocks, each a
+        distributed matrix of its own on this grid in the standard layout; block
+        sizes as the reference's (the first n % b blocks one longer).  A row
+        split (bc = 1) or a column split (br = 1) -- the splits BlockSpGEMM makes
+        (BlockSpGEMM.h:39-45) -- is one collective per block; a 2-D split is
+        the row split's blocks split by columns."""
+        if (br == 1 and bc == 1) or br > self.gm or bc > self.gn:
+            return [[self]]
+        roff = _block_offsets(self.gm, br)
+        coff = _block_offsets(self.gn, bc)
+        rows = [self._block_extract(0, roff[i], roff[i + 1]) if br > 1 else self for i in range(br)]
+        out = []
+        for R in rows:
+            out.append([R._block_extract(1, coff[j], coff[j + 1]) if bc > 1 else R for j in range(bc)])
+            if bc > 1 and R is not self:
+                R.tile.free()
+        return out
+
     def DimApply(self, dim, vec, op="multiplies"):
         """SpParMat::DimApply (SpParMat.cpp:801) with a dense global vector (host array of
         ncol (Column) or nrow (Row) values); each rank applies its block's slice."""
@@ -779,6 +806,48 @@ def MemEfficientSpGEMM(A, B, phases, sr=PlusTimesSRing, algo=DOUBLEBUFF, exec_mo
         raise errors[0]
     _check(rc)
     return SpParMat(C, A.grid, A.gm, B.gn) if C is not None else None
+
+
+def _block_offsets(n, nb):
+    """block starts of BlockSplit / BlockSpGEMM::getBlockOffsets (BlockSpGEMM.h:114-131):
+    n // nb per block, the first n % nb blocks one longer; n at the end."""
+    bs, r = divmod(n, nb)
+    return [min(b, r) * (bs + 1) + max(b - r, 0) * bs for b in range(nb)] + [n]
+
+
+class BlockSpGEMM:
+    """BlockSpGEMM (BlockSpGEMM.h:14-131): C = A*B computed block by block.  A is
+    split into br row blocks, B into bc column blocks (bi = 1, as the reference
+    asserts); getNextBlock() multiplies the next (row block, column block) pair
+    with Mult_AnXBn_DoubleBuff and returns the C block with its global row and
+    column offsets.  Collective over A's grid."""
+
+    def __init__(self, A, B, br, bc, bi=1):
+        if bi != 1:
+            raise CbgError(NOTSUPPORTED, "BlockSpGEMM with bi != 1 (the reference asserts bi == 1)")
+        self.br, self.bc, self.bi, self.cur_block = br, bc, bi, 0
+        self.A_blocks = A.BlockSplit(br, bi)
+        self.B_blocks = B.BlockSplit(bi, bc)
+        self.nr, self.nc = A.getnrow(), B.getncol()
+
+    def hasNext(self):
+        return self.cur_block < self.br * self.bc
+
+    def getBlockOffsets(self, is_row):
+        return _block_offsets(self.nr, self.br) if is_row else _block_offsets(self.nc, self.bc)
+
+    def getBlockId(self, rbid, cbid, sr=PlusTimesSRing):
+        """-> (C block, roffset, coffset)"""
+        roff = _block_offsets(self.nr, self.br)[rbid]
+        coff = _block_offsets(self.nc, self.bc)[cbid]
+        C = Mult_AnXBn_DoubleBuff(self.A_blocks[rbid][0], self.B_blocks[0][cbid], sr)
+        return C, roff, coff
+
+    def getNextBlock(self, sr=PlusTimesSRing):
+        """-> (C block, roffset, coffset) of block cur_block (row-major over the blocks)"""
+        rbid, cbid = divmod(self.cur_block, self.bc)
+        self.cur_block += 1
+        return self.getBlockId(rbid, cbid, sr)
 
 
 def PSpGEMM(A, B, sr=PlusTimesSRing):

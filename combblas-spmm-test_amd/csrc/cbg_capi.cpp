@@ -23,6 +23,8 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                         int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C);
 int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out);
+int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, int dim, int64_t lo, int64_t hi,
+                       cbg_tile& out);
 }  // namespace cbg
 
 namespace {
@@ -223,6 +225,19 @@ int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out) {
     CBG_HIP(hipDeviceSynchronize());
     int rc = cbg::grid_transpose(g, *local, *out);
     if (rc) return fail(rc, "SpParMat::Transpose needs a square grid");
+    return CBG_OK;
+  });
+}
+
+int cbg_grid_block_extract(cbg_grid* g, const cbg_tile* local, int64_t gm, int64_t gn, int dim, int64_t lo,
+                           int64_t hi, cbg_tile* out) {
+  if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
+  if (int rc = check_tile(local, true, "tile")) return rc;
+  if (!out) return fail(CBG_ERR_INVALIDPARAMS, "out is NULL");
+  return guard([&]() -> int {
+    CBG_HIP(hipDeviceSynchronize());
+    int rc = cbg::grid_block_extract(g, *local, gm, gn, dim, lo, hi, *out);
+    if (rc) return fail(rc, "block range outside the matrix or bad dim");
     return CBG_OK;
   });
 }

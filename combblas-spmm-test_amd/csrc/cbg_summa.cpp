@@ -472,6 +472,88 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
   return CBG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// SpParMat::BlockSplit (SpParMat.cpp:2974-3058) for the splits BlockSpGEMM
+// uses (bi = 1, BlockSpGEMM.h:39-45): global rows [lo, hi) of a distributed
+// matrix (dim 0) or columns [lo, hi) (dim 1) as a distributed matrix of its
+// own on the same grid, in the standard block layout (Owner,
+// SpParMat.cpp:5068-5097).  Rows only move inside a grid column (columns
+// inside a grid row): every rank broadcasts its slice of the range to its
+// column (row) communicator and keeps the part of each slice that falls in
+// its new block.
+// ---------------------------------------------------------------------------
+int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, int dim, int64_t lo, int64_t hi,
+                       cbg_tile& out) {
+  if (dim != 0 && dim != 1) return CBG_ERR_INVALIDPARAMS;
+  const int64_t gext = dim == 0 ? gm : gn;
+  if (lo < 0 || hi < lo || hi > gext) return CBG_ERR_INVALIDPARAMS;
+  hipStream_t cs = g->compute;
+  const int which = dim == 0 ? COMM_COL : COMM_ROW;
+  const int np = comm_size(g, which), me = comm_rank(g, which);
+  // my old range [S0, S1) along dim and my new range [lo + T0, lo + T1)
+  auto span = [](int64_t ext, int np_, int i, int64_t& a, int64_t& b) {
+    const int64_t per = ext / np_;
+    a = (int64_t)i * per;
+    b = i == np_ - 1 ? ext : a + per;
+  };
+  int64_t S0, S1, T0, T1;
+  span(gext, np, me, S0, S1);
+  span(hi - lo, np, me, T0, T1);
+  T0 += lo;
+  T1 += lo;
+  auto cut = [&](const cbg_tile& X, int64_t a, int64_t b, cbg_tile& piece) {  // local range [a, b) of X
+    cbg_tile head{}, rest{}, tail{};
+    if (dim == 0) {
+      tile_split_rows(X, b, head, tail, cs);
+      tile_free_device(tail);
+      tile_split_rows(head, a, rest, piece, cs);
+    } else {
+      tile_split_cols(X, b, head, tail, cs);
+      tile_free_device(tail);
+      tile_split_cols(head, a, rest, piece, cs);
+    }
+    tile_free_device(rest);
+    tile_free_device(head);
+  };
+  // my slice of [lo, hi)
+  const int64_t x0 = std::max(S0, lo), x1 = std::max(x0, std::min(S1, hi));
+  cbg_tile mine{};
+  cut(T, x0 - S0, x1 - S0, mine);
+  int64_t e[4] = {mine.m, mine.n, mine.nnz, mine.nzc};
+  std::vector<int64_t> E((size_t)4 * np);
+  allgather_i64(g, which, e, E.data(), 4);
+  std::vector<cbg_tile> parts;
+  std::vector<int64_t> offs;
+  for (int q = 0; q < np; ++q) {
+    int64_t Q0, Q1;
+    span(gext, np, q, Q0, Q1);
+    const int64_t y0 = std::max(Q0, lo), y1 = std::max(y0, std::min(Q1, hi));  // slice of rank q
+    cbg_tile sl = q == me ? mine : cbg_tile{};
+    bcast_tile(g, which, q, &E[4 * (size_t)q], sl, q == me);
+    CBG_HIP(hipStreamSynchronize(g->comm));
+    const int64_t z0 = std::max(y0, T0), z1 = std::min(y1, T1);  // the part of it in my new range
+    if (z1 > z0) {
+      cbg_tile piece{};
+      cut(sl, z0 - y0, z1 - y0, piece);
+      parts.push_back(piece);
+      offs.push_back(z0 - T0);
+    }
+    if (q != me) tile_free_device(sl);
+  }
+  tile_free_device(mine);
+  const int64_t om = dim == 0 ? T1 - T0 : T.m, on = dim == 0 ? T.n : T1 - T0;
+  if (parts.empty()) {
+    tile_alloc_device(out, om, on, 0, 0);
+  } else if (dim == 0) {
+    tile_concat_rows(parts, offs, om, on, out, cs);
+  } else {
+    tile_concat_cols(parts, offs, om, on, out, cs);
+  }
+  for (auto& t : parts) tile_free_device(t);
+  CBG_HIP(hipStreamSynchronize(cs));
+  return CBG_OK;
+}
+
 }  // namespace cbg
 
 extern "C" int cbg_get_unique_id(void* id) {

@@ -193,6 +193,15 @@ int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile
  * on non-square grids, like the reference. */
 int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out);
 
+/* SpParMat::BlockSplit (SpParMat.cpp:2974-3058) as BlockSpGEMM uses it
+ * (BlockSpGEMM.h:39-45, bi = 1), collective over the grid: the global rows
+ * [lo, hi) (dim 0) or columns [lo, hi) (dim 1) of the gm x gn distributed
+ * matrix whose local tile is `local`, as a distributed matrix of their own on
+ * the same grid (standard block layout, SpParMat::Owner SpParMat.cpp:5068);
+ * out = this rank's tile of it. */
+int cbg_grid_block_extract(cbg_grid* g, const cbg_tile* local, int64_t gm, int64_t gn, int dim, int64_t lo,
+                           int64_t hi, cbg_tile* out);
+
 #ifdef __cplusplus
 }
 #endif

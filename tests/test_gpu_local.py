@@ -492,3 +492,46 @@ def test_cpp_galerkin_driver():
     r = subprocess.run([exe, "12", "2"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "Splitting approach is correct" in r.stdout
+
+
+def _self_grid_1x1(cbg):
+    class Self:
+        def bcast(self, comm, arr, root):
+            pass
+
+        def allgather(self, comm, data):
+            return data
+
+    return cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+
+
+def test_block_split_and_blockspgemm(cbg):
+    """SpParMat::BlockSplit (SpParMat.cpp:2974-3058) and BlockSpGEMM (BlockSpGEMM.h):
+    blocks are the reference's sub-matrices (first n % b blocks one longer), and the
+    C blocks at their offsets tile the golden A*A exactly (ReleaseTests/BlockedSpGEMM.cpp)."""
+    from helpers import load_npz
+    g = _self_grid_1x1(cbg)
+    Ah = load_npz("rmat_s10_ef16_A.npz")
+    Ch = load_npz("rmat_s10_ef16_C_local_plus.npz")
+    A = cbg.SpParMat.from_global(g, Ah)
+    B = cbg.SpParMat.from_global(g, Ah)
+    blocks = A.BlockSplit(3, 2)
+    roff, coff = cbg._block_offsets(Ah["m"], 3), cbg._block_offsets(Ah["n"], 2)
+    assert roff == [0, 342, 683, 1024] and coff == [0, 512, 1024]
+    for i in range(3):
+        for j in range(2):
+            assert_tiles_equal(blocks[i][j].tile.to_host(), cbg.sub_tile(Ah, roff[i], roff[i + 1], coff[j], coff[j + 1]))
+    bs = cbg.BlockSpGEMM(A, B, 3, 2)
+    assert bs.getBlockOffsets(True) == roff and bs.getBlockOffsets(False) == coff
+    seen = 0
+    while bs.hasNext():
+        C, r0, c0 = bs.getNextBlock()
+        rb, cb = roff.index(r0), coff.index(c0)
+        assert (C.getnrow(), C.getncol()) == (roff[rb + 1] - r0, coff[cb + 1] - c0)
+        assert_tiles_equal(C.tile.to_host(), cbg.sub_tile(Ch, r0, roff[rb + 1], c0, coff[cb + 1]))
+        seen += 1
+    assert seen == 6
+    C, r0, c0 = bs.getBlockId(2, 1)
+    assert (r0, c0) == (683, 512)
+    assert A.BlockSplit(1, 1)[0][0] is A
+    g.destroy()

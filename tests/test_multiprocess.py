@@ -73,3 +73,12 @@ def test_galerkin_multiprocess_gpu(grid):
     """GalerkinNew on a 2x2 grid: distributed Transpose + PSpGEMM + DimApply + += (host transport)."""
     rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "galerkin"], timeout=600)
     assert rc == 0 and "MPOK" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(2, 1), (1, 2), (2, 2)])
+def test_blockspgemm_multiprocess_gpu(grid):
+    """BlockedSpGEMM: BlockSplit's redistribution of row / column blocks over a grid and
+    the block products, checked against the golden A*A digest (host transport)."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "blockspgemm"], timeout=600)
+    assert rc == 0 and "MPOK" in out, out[-3000:]
