@@ -341,6 +341,38 @@ class SpParMat {
     return SpParMat(new DER(t), g, n, n / order);
   }
 
+  // rows (dim 0) or columns (dim 1) [lo, hi) as a distributed matrix of their own
+  SpParMat BlockExtract(int dim, IT lo, IT hi) const {
+    cbg_tile t{};
+    cbg_abort_on(cbg_grid_block_extract(commGrid->handle(), spSeq->tile(), m_, n_, dim, lo, hi, &t), "BlockSplit");
+    return SpParMat(new DER(t), commGrid, dim == 0 ? hi - lo : m_, dim == 1 ? hi - lo : n_);
+  }
+  // block starts of BlockSplit / BlockSpGEMM::getBlockOffsets: n / nb per
+  // block, the first n % nb blocks one longer, n at the end
+  static std::vector<IT> BlockOffsets(IT n, int nb) {
+    std::vector<IT> o(nb + 1);
+    const IT bs = n / nb, r = n % nb;
+    for (int b = 0; b < nb; ++b) o[b] = std::min((IT)b, r) * (bs + 1) + ((IT)b < r ? 0 : (IT)b - r) * bs;
+    o[nb] = n;
+    return o;
+  }
+  // SpParMat::BlockSplit (SpParMat.cpp:2974-3058): br x bc blocks, each a
+  // distributed matrix on this grid in the standard layout
+  std::vector<std::vector<SpParMat>> BlockSplit(int br, int bc) const {
+    std::vector<std::vector<SpParMat>> out(br);
+    if ((br == 1 && bc == 1) || (IT)br > m_ || (IT)bc > n_) {
+      out.resize(1);
+      out[0].push_back(BlockExtract(0, 0, m_));  // a copy of *this
+      return out;
+    }
+    const std::vector<IT> ro = BlockOffsets(m_, br), co = BlockOffsets(n_, bc);
+    for (int i = 0; i < br; ++i) {
+      SpParMat R = BlockExtract(0, ro[i], ro[i + 1]);
+      for (int j = 0; j < bc; ++j) out[i].push_back(bc == 1 ? std::move(R) : R.BlockExtract(1, co[j], co[j + 1]));
+    }
+    return out;
+  }
+
   // SpParMat::operator== (SpParMat.cpp:2878-2884): local equality, AND over the grid
   bool operator==(const SpParMat& rhs) const {
     int64_t bad = (*spSeq == *rhs.spSeq) ? 0 : 1;
@@ -420,6 +452,43 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMa
                "MemEfficientSpGEMM");
   return SpParMat<IU, NUO, UDERO>(new UDERO(c), A.commGrid, A.getnrow(), B.getncol());
 }
+
+// BlockSpGEMM (BlockSpGEMM.h:14-131): C = A*B block by block, A split into br
+// row blocks and B into bc column blocks (bi = 1), each block product a
+// Mult_AnXBn_DoubleBuff
+template <typename IT, typename NTA, typename DERA, typename NTB, typename DERB>
+struct BlockSpGEMM {
+  BlockSpGEMM(SpParMat<IT, NTA, DERA>& A, SpParMat<IT, NTB, DERB>& B, int br, int bc, int bi = 1)
+      : br_(br), bc_(bc), bi_(bi), cur_block_(0) {
+    if (bi_ != 1) cbg_abort_on(CBG_ERR_NOTSUPPORTED, "BlockSpGEMM: bi must be 1");
+    A_blocks_ = A.BlockSplit(br_, bi_);
+    B_blocks_ = B.BlockSplit(bi_, bc_);
+    nr_ = A.getnrow();
+    nc_ = B.getncol();
+  }
+  template <typename SR, typename NTC, typename DERC>
+  SpParMat<IT, NTC, DERC> getNextBlock(IT& roffset, IT& coffset) {
+    const int rbid = cur_block_ / bc_, cbid = cur_block_ % bc_;
+    ++cur_block_;
+    return getBlockId<SR, NTC, DERC>(rbid, cbid, roffset, coffset);
+  }
+  bool hasNext() { return cur_block_ < br_ * bc_; }
+  template <typename SR, typename NTC, typename DERC>
+  SpParMat<IT, NTC, DERC> getBlockId(int rbid, int cbid, IT& roffset, IT& coffset) {
+    roffset = getBlockOffsets(true)[rbid];
+    coffset = getBlockOffsets(false)[cbid];
+    return Mult_AnXBn_DoubleBuff<SR, NTC, DERC>(A_blocks_[rbid][0], B_blocks_[0][cbid], false, false);
+  }
+  std::vector<IT> getBlockOffsets(bool is_row) {
+    return SpParMat<IT, NTA, DERA>::BlockOffsets(is_row ? nr_ : nc_, is_row ? br_ : bc_);
+  }
+
+ private:
+  std::vector<std::vector<SpParMat<IT, NTA, DERA>>> A_blocks_;
+  std::vector<std::vector<SpParMat<IT, NTB, DERB>>> B_blocks_;
+  int br_, bc_, bi_, cur_block_;
+  IT nr_ = 0, nc_ = 0;
+};
 
 // SpParMat.h:454-467
 template <typename SR, typename IU, typename NU1, typename NU2, typename UDERA, typename UDERB>

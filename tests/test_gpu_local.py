@@ -535,3 +535,24 @@ def test_block_split_and_blockspgemm(cbg):
     assert (r0, c0) == (683, 512)
     assert A.BlockSplit(1, 1)[0][0] is A
     g.destroy()
+
+
+def test_cpp_blockedspgemm_driver():
+    """tools/blockedspgemm (ReleaseTests/BlockedSpGEMM.cpp on the C++ mirror header): the
+    reference's per-block lines, and the blocks' nonzeros add up to nnz(A*B)."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "tools", "blockedspgemm")
+    if not os.path.exists(exe):
+        pytest.skip("tools/blockedspgemm not built (needs MPICH in /opt/conda)")
+    mm = os.path.join(repo, "tests", "golden", "sevenvertex.mtx")
+    r = subprocess.run([exe, mm, mm, "2", "3"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.splitlines()  # (RCCL may print a banner first)
+    assert any(ln.startswith("A 7 7 12") for ln in lines) and any(ln.startswith("B 7 7 12") for ln in lines)
+    blocks = [ln.split() for ln in lines if ln.startswith("block size")]
+    assert [(b[2], b[3], b[6], b[7]) for b in blocks] == [("4", "3", "0", "0"), ("4", "2", "0", "3"),
+                                                         ("4", "2", "0", "5"), ("3", "3", "4", "0"),
+                                                         ("3", "2", "4", "3"), ("3", "2", "4", "5")]
+    assert "BlockSpGEMM blocks cover A*B" in r.stdout
