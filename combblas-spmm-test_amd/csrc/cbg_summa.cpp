@@ -377,7 +377,11 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
   for (int p = 0; p < phases; ++p) off[p] = (int64_t)p * w;
   std::vector<cbg_tile> parts;
   int cb_rc = 0;
-  APrepScope aprep_scope;  // every phase multiplies the same A
+  // every phase multiplies the caller's A itself when the PANEL execution needs
+  // no A row concatenation (one grid column): keep its column maps across the
+  // phases (other executions multiply per-stage / per-phase copies of A)
+  std::unique_ptr<APrepScope> aprep_scope;
+  if (exec == CBG_EXEC_PANEL && g->pc == 1) aprep_scope.reset(new APrepScope());
   for (int p = 0; p < phases; ++p) {
     cbg_tile Cp{};
     const int rc = summa_spgemm(g, A, pieces[p], A_gncol, B_gnrow, sr, algo, exec, Cp);
