@@ -556,3 +556,22 @@ def test_cpp_blockedspgemm_driver():
                                                          ("4", "2", "0", "5"), ("3", "3", "4", "0"),
                                                          ("3", "2", "4", "3"), ("3", "2", "4", "5")]
     assert "BlockSpGEMM blocks cover A*B" in r.stdout
+
+
+@pytest.mark.parametrize("scale", [20, 21])
+def test_local_digest_large_vs_oracle(cbg, scale):
+    """R-MAT 20/21 (4 and 8 row panels: panel groups, multi-slab pairs) against the
+    oracle's digests (tests/golden/oracle_large.json, made by tools/check_scale.py)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        g = json.load(f)[f"s{scale}_ef16"]
+    A = cbg.rmat_tile(scale, 16)
+    B = cbg.rmat_tile(scale, 16)
+    C = cbg.LocalHybridSpGEMM(A, B)
+    d = C.digest()
+    C.free()
+    assert d["nnz"] == g["nnz"] and d["nzc"] == g["nzc"] and d["hs"] == g["hs"] and d["hv"] == g["hv"], (d, g)
+    sym = G["rmat"].get(f"s{scale}_ef16", {}).get("symbolic")
+    if sym:  # the reference's own symbolic total
+        assert d["nnz"] == sym["nnzC"]
