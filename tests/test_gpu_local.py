@@ -558,17 +558,17 @@ def test_cpp_blockedspgemm_driver():
     assert "BlockSpGEMM blocks cover A*B" in r.stdout
 
 
-@pytest.mark.parametrize("scale", [20, 21])
-def test_local_digest_large_vs_oracle(cbg, scale):
+@pytest.mark.parametrize("scale,sr", [(20, "plus"), (21, "plus"), (20, "minplus")])
+def test_local_digest_large_vs_oracle(cbg, scale, sr):
     """R-MAT 20/21 (4 and 8 row panels: panel groups, multi-slab pairs) against the
     oracle's digests (tests/golden/oracle_large.json, made by tools/check_scale.py)."""
     import json
     import os
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
-        g = json.load(f)[f"s{scale}_ef16"]
+        g = json.load(f)[f"s{scale}_ef16" + ("" if sr == "plus" else "_" + sr)]
     A = cbg.rmat_tile(scale, 16)
     B = cbg.rmat_tile(scale, 16)
-    C = cbg.LocalHybridSpGEMM(A, B)
+    C = cbg.LocalHybridSpGEMM(A, B, sr)
     d = C.digest()
     C.free()
     assert d["nnz"] == g["nnz"] and d["nzc"] == g["nzc"] and d["hs"] == g["hs"] and d["hv"] == g["hv"], (d, g)

@@ -54,6 +54,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=20)
     p.add_argument("--threads", type=int, default=16)
+    p.add_argument("--sr", choices=["plus", "minplus"], default="plus")
     a = p.parse_args()
     from conftest import load_cbg
     cbg = load_cbg()
@@ -61,7 +62,7 @@ def main():
     t0 = time.time()
     A = cbg.rmat_tile(a.scale, 16)
     B = cbg.rmat_tile(a.scale, 16)
-    C = cbg.LocalHybridSpGEMM(A, B)
+    C = cbg.LocalHybridSpGEMM(A, B, a.sr)
     gd = C.digest()
     C.free()
     A.free()
@@ -70,7 +71,7 @@ def main():
     from helpers import oracle_local, oracle_rmat  # the checker
     t0 = time.time()
     Ah = oracle_rmat(a.scale, 16, nthreads=a.threads)
-    Ch = oracle_local(Ah, dict(Ah), nthreads=a.threads)
+    Ch = oracle_local(Ah, dict(Ah), a.sr, nthreads=a.threads)
     print(json.dumps({"oracle_s": round(time.time() - t0, 1), "nnz": int(len(Ch["ir"]))}), flush=True)
     od = chunked_digest(Ch)
     ok = od["nnz"] == gd["nnz"] and od["hs"] == gd["hs"] and od["hv"] == gd["hv"] and od["unsorted"] == 0
