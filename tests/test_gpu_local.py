@@ -575,3 +575,28 @@ def test_local_digest_large_vs_oracle(cbg, scale, sr):
     sym = G["rmat"].get(f"s{scale}_ef16", {}).get("symbolic")
     if sym:  # the reference's own symbolic total
         assert d["nnz"] == sym["nnzC"]
+
+
+def test_phased_scale22_vs_oracle(cbg):
+    """The bench's configuration: R-MAT scale-22 A*A as MemEfficientSpGEMM with 4
+    B-column phases on one GPU, each phase's C digested on the device as it is
+    streamed; the sum equals the oracle's digest of the whole C (24.8 G nonzeros,
+    tests/golden/oracle_large.json) and nnz the reference's symbolic total."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        g = json.load(f)["s22_ef16"]
+    grid = _self_grid_1x1(cbg)
+    nv = 1 << 22
+    A = cbg.SpParMat(cbg.rmat_tile(22, 16), grid, nv, nv)
+    B = cbg.SpParMat(cbg.rmat_tile(22, 16), grid, nv, nv)
+    parts = []
+    cbg.MemEfficientSpGEMM(A, B, 4, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)))
+    hs = "%016x" % (sum(int(d["hs"], 16) for d in parts) % (1 << 64))
+    hv = "%016x" % (sum(int(d["hv"], 16) for d in parts) % (1 << 64))
+    nnz = sum(d["nnz"] for d in parts)
+    A.tile.free()
+    B.tile.free()
+    grid.destroy()
+    assert (nnz, hs, hv) == (g["nnz"], g["hs"], g["hv"])
+    assert nnz == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"]
