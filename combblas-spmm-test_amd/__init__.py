@@ -659,6 +659,14 @@ class SpParMat:
         return SpParMat(t, grid, nv, nv)
 
     @staticmethod
+    def ReadDistribute(grid, filename, master=0):
+        """SpParMat::ReadDistribute (SpParMat.cpp:4211-4540), text or HKDT binary
+        triples: every rank parses the file and keeps its block of the block
+        distribution (the reference's master reads and scatters; the tiles are
+        the same)."""
+        return SpParMat.from_global(grid, read_triples(filename))
+
+    @staticmethod
     def ParallelReadMM(grid, filename, onebased=True, binop="max"):
         """SpParMat::ParallelReadMM (SpParMat.cpp:3980-4117): every rank parses the
         file and keeps its block of the block distribution (the reference splits
@@ -676,6 +684,66 @@ class SpParMat:
 
 
 _BINOPS = {"max": np.maximum, "min": np.minimum, "plus": np.add, "first": None}
+
+
+def _dcsc_from_triples(m, n, rows, cols, vals):
+    """tuples -> global host DCSC dict sorted by (col, row) (SpTuples::SortColBased;
+    stable, so duplicates keep their file order), duplicates kept like
+    SpDCCols::Create(size, m, n, tuples) (SpDCCols.cpp:748)."""
+    order = np.lexsort((rows, cols))
+    rows, cols, vals = rows[order], cols[order], vals[order]
+    jc, start = np.unique(cols, return_index=True)
+    return dict(m=int(m), n=int(n), cp=np.append(start, len(rows)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=rows.astype(np.int32), val=vals.astype(np.float64))
+
+
+def read_triples(path):
+    """The files of SpParMat::ReadDistribute (SpParMat.cpp:4211-4540) -> global host
+    DCSC dict.  Text: '%' comment lines, then "m n nnz", then nnz lines "i j [v]"
+    (1-based; a missing value reads as 1, ScalarReadSaveHandler::getNoNum).
+    Binary (FileHeader.h ParseHeader): "HKDT", uint64 version, objsize, format, m,
+    n, nnz, then nnz records {int64 row, int64 col, double val} (0-based,
+    binaryfill, SpParMat.h:250-260)."""
+    with open(path, "rb") as f:
+        head = f.read(4)
+        if head == b"HKDT":
+            version, objsize, fmt, m, n, nnz = np.frombuffer(f.read(48), dtype=np.uint64).tolist()
+            if fmt != 0:
+                raise CbgError(INVALIDPARAMS, f"{path}: Ascii input with binary headers is not supported")
+            rec = np.dtype([("r", "<i8"), ("c", "<i8"), ("v", "<f8")])
+            t = np.frombuffer(f.read(int(nnz) * rec.itemsize), dtype=rec, count=int(nnz))
+            return _dcsc_from_triples(m, n, t["r"].astype(np.int64), t["c"].astype(np.int64),
+                                      t["v"].astype(np.float64))
+    with open(path) as f:
+        line = f.readline()
+        while line.startswith("%"):
+            line = f.readline()
+        m, n, nnz = (int(x) for x in line.split()[:3])
+        rows = np.empty(nnz, np.int64)
+        cols = np.empty(nnz, np.int64)
+        vals = np.ones(nnz, np.float64)
+        for k in range(nnz):
+            parts = f.readline().split()
+            rows[k] = int(parts[0]) - 1
+            cols[k] = int(parts[1]) - 1
+            if len(parts) > 2:
+                vals[k] = float(parts[2])
+    return _dcsc_from_triples(m, n, rows, cols, vals)
+
+
+def read_vector(path):
+    """FullyDistVec::ReadDistribute (FullyDistVec.cpp:495 -> FullyDistSpVec.cpp:1397-1437)
+    -> dense host vector: header "m n nnz", then "i j v" lines (1-based); the index
+    is the row for a column vector (n == 1), else the column; absent entries are 0."""
+    with open(path) as f:
+        m, n, nnz = (int(x) for x in f.readline().split()[:3])
+        glen = m if n == 1 else n
+        out = np.zeros(glen, np.float64)
+        for _ in range(nnz):
+            parts = f.readline().split()
+            i = int(parts[0] if n == 1 else parts[1]) - 1
+            out[i] = float(parts[2]) if len(parts) > 2 else 1.0
+    return out
 
 
 def read_mm(path, onebased=True, binop="max"):

@@ -54,3 +54,43 @@ def test_symmetric_pattern_duplicates(tmp_path):
     p.write_text("%%MatrixMarket matrix coordinate real general\n3 3 0\n")
     d = cbg.read_mm(str(p))
     assert d["m"] == 3 and len(d["ir"]) == 0 and len(d["cp"]) == 1
+
+
+def test_read_distribute_matches_reference():
+    """SpParMat::ReadDistribute triples files (data files of the reference's tests:
+    ReleaseTests/small_nonsym.mtx, largeseq/input{1,2}_0) read to exactly the
+    tiles the reference's own ReadDistribute produced (golden *_A/_B.npz, made by
+    oracle/_ref readtriples)."""
+    cbg = load_cbg()
+    for f, g in (("small_nonsym.triples", "small_nonsym_A.npz"), ("largeseq_input1_0.triples", "largeseq_A.npz"),
+                 ("largeseq_input2_0.triples", "largeseq_B.npz")):
+        d = cbg.read_triples(os.path.join(GOLD, f))
+        r = load_npz(g)
+        assert (d["m"], d["n"]) == (r["m"], r["n"]), f
+        for k in ("cp", "jc", "ir", "val"):
+            assert np.array_equal(d[k], r[k]), (f, k)
+
+
+def test_read_distribute_binary_and_nonum(tmp_path):
+    """HKDT binary triples (FileHeader.h, 0-based int64/int64/double records) and
+    text lines without a value (read as 1, ScalarReadSaveHandler::getNoNum)."""
+    cbg = load_cbg()
+    r = cbg.read_triples(os.path.join(GOLD, "largeseq_input1_0.triples"))
+    cols = np.repeat(r["jc"].astype(np.int64), np.diff(r["cp"]))
+    rec = np.zeros(len(cols), dtype=[("r", "<i8"), ("c", "<i8"), ("v", "<f8")])
+    rec["r"], rec["c"], rec["v"] = r["ir"], cols, r["val"]
+    p = tmp_path / "b.bin"
+    with open(p, "wb") as f:
+        f.write(b"HKDT")
+        f.write(np.array([1, 24, 0, r["m"], r["n"], len(cols)], np.uint64).tobytes())
+        f.write(rec[np.random.default_rng(0).permutation(len(rec))].tobytes())
+    b = cbg.read_triples(str(p))
+    for k in ("cp", "jc", "ir", "val"):
+        assert np.array_equal(b[k], r[k]), k
+    q = tmp_path / "t.txt"
+    q.write_text("% c\n3 3 3\n1 1\n3 2 5.5\n2 2\n")
+    d = cbg.read_triples(str(q))
+    assert dense(d).tolist() == [[1, 0, 0], [0, 1, 0], [0, 5.5, 0]]
+    v = tmp_path / "v.txt"
+    v.write_text("4 1 2\n2 1 0.5\n4 1 -3\n")
+    assert cbg.read_vector(str(v)).tolist() == [0, 0.5, 0, -3]
