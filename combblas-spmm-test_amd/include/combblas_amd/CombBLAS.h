@@ -13,6 +13,8 @@
 //   MemEfficientSpGEMM         ParFriends.h:449   MemEfficientSpGEMM (phases; no MCL pruning)
 //   SpParMat::Transpose        SpParMat.cpp:3528  Transpose (square grids, RCCL send/recv)
 //   SpParMat::DimApply         SpParMat.cpp:801   DimApply (dense vector given as its global values)
+//   SpParMat::ReadDistribute   SpParMat.cpp:4211  ReadDistribute (text / HKDT binary triples)
+//   FullyDistVec::ReadDistribute FullyDistVec.cpp:495 ReadDistributeVector (global values)
 //   SpParMat::operator+=       SpParMat.cpp:741   operator+= (device merge)
 //   SpDCCols/SpParMat ==       SpDCCols.h:74, SpParMat.cpp:2878  operator== (ErrorTolerantEqual)
 //
@@ -296,6 +298,67 @@ class SpParMat {
     n_ = (IT)n;
   }
 
+  // SpParMat::ReadDistribute (SpParMat.cpp:4211-4540), the GalerkinNew input:
+  // text = '%' comment lines, "m n nnz", then nnz lines "i j [v]" (1-based, a
+  // missing value reads 1); binary = "HKDT" + uint64 {version, objsize, format, m,
+  // n, nnz} + nnz {int64 row, int64 col, double val} records (0-based).  Tuples
+  // sorted column-major, duplicates kept (SpDCCols::Create).  Every rank reads
+  // the file and keeps its block; the master argument is accepted for the
+  // reference's signature.
+  void ReadDistribute(const std::string& filename, int master = 0) {
+    (void)master;
+    FILE* f = std::fopen(filename.c_str(), "rb");
+    if (!f) cbg_abort_on(3004, ("ReadDistribute: file " + filename + " can not be found").c_str());  // NOFILE
+    long long m = 0, n = 0, nz = 0;
+    std::vector<long long> ri, ci;
+    std::vector<double> vv;
+    char magic[4] = {0};
+    if (std::fread(magic, 1, 4, f) == 4 && std::memcmp(magic, "HKDT", 4) == 0) {
+      uint64_t h[6];
+      if (std::fread(h, sizeof h, 1, f) != 1 || h[2] != 0)
+        cbg_abort_on(CBG_ERR_INVALIDPARAMS, "ReadDistribute: bad binary header");
+      m = (long long)h[3];
+      n = (long long)h[4];
+      nz = (long long)h[5];
+      struct Rec { int64_t r, c; double v; } rec;
+      for (long long k = 0; k < nz && std::fread(&rec, sizeof rec, 1, f) == 1; ++k) {
+        ri.push_back(rec.r);
+        ci.push_back(rec.c);
+        vv.push_back(rec.v);
+      }
+    } else {
+      std::rewind(f);
+      char line[1024];
+      while (std::fgets(line, sizeof line, f))
+        if (line[0] != '%' && std::sscanf(line, "%lld %lld %lld", &m, &n, &nz) == 3) break;
+      for (long long k = 0; k < nz && std::fgets(line, sizeof line, f); ++k) {
+        long long i, j;
+        double v = 1.0;
+        if (std::sscanf(line, "%lld %lld %lg", &i, &j, &v) < 2) { --k; continue; }
+        ri.push_back(i - 1);
+        ci.push_back(j - 1);
+        vv.push_back(v);
+      }
+    }
+    std::fclose(f);
+    const int pr = commGrid->GetGridRows(), pc = commGrid->GetGridCols();
+    const int r = commGrid->GetRankInProcCol(), c = commGrid->GetRankInProcRow();
+    const long long mper = m / pr, nper = n / pc;  // SpParMat::Owner (SpParMat.cpp:5068-5097)
+    const long long r0 = r * mper, r1 = (r == pr - 1) ? m : r0 + mper;
+    const long long c0 = c * nper, c1 = (c == pc - 1) ? n : c0 + nper;
+    std::vector<std::tuple<IT, IT, NT>> t;
+    for (size_t k = 0; k < ri.size(); ++k)
+      if (ri[k] >= r0 && ri[k] < r1 && ci[k] >= c0 && ci[k] < c1)
+        t.emplace_back((IT)(ri[k] - r0), (IT)(ci[k] - c0), (NT)vv[k]);
+    std::stable_sort(t.begin(), t.end(), [](const std::tuple<IT, IT, NT>& a, const std::tuple<IT, IT, NT>& b) {
+      return std::get<1>(a) != std::get<1>(b) ? std::get<1>(a) < std::get<1>(b) : std::get<0>(a) < std::get<0>(b);
+    });
+    delete spSeq;
+    spSeq = new DER((IT)(r1 - r0), (IT)(c1 - c0), (IT)t.size(), t.data(), false);
+    m_ = (IT)m;
+    n_ = (IT)n;
+  }
+
   IT getnrow() const { return m_; }
   IT getncol() const { return n_; }
   int64_t getnnz() const {  // SpParMat::getnnz (Allreduce, SpParMat.cpp:772-778)
@@ -494,6 +557,29 @@ struct BlockSpGEMM {
 template <typename SR, typename IU, typename NU1, typename NU2, typename UDERA, typename UDERB>
 SpParMat<IU, typename SR::T_promote, UDERA> PSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B) {
   return Mult_AnXBn_Synch<SR, typename SR::T_promote, UDERA>(A, B);
+}
+
+// FullyDistVec<IT,double>::ReadDistribute (FullyDistVec.cpp:495 ->
+// FullyDistSpVec.cpp:1397-1437) as the global values DimApply takes: header
+// "m n nnz", then "i j v" lines (1-based); the index is the row of a column
+// vector (n == 1), else the column; absent entries are 0.
+inline std::vector<double> ReadDistributeVector(const std::string& filename) {
+  FILE* f = std::fopen(filename.c_str(), "r");
+  if (!f) cbg_abort_on(3004, ("ReadDistribute: file " + filename + " can not be found").c_str());  // NOFILE
+  char line[1024];
+  long long m = 0, n = 0, nz = 0;
+  if (!std::fgets(line, sizeof line, f) || std::sscanf(line, "%lld %lld %lld", &m, &n, &nz) != 3)
+    cbg_abort_on(CBG_ERR_INVALIDPARAMS, "ReadDistribute: bad vector header");
+  std::vector<double> out((size_t)(n == 1 ? m : n), 0.0);
+  for (long long k = 0; k < nz && std::fgets(line, sizeof line, f); ++k) {
+    long long i, j;
+    double v = 1.0;
+    if (std::sscanf(line, "%lld %lld %lg", &i, &j, &v) < 2) continue;
+    const long long x = (n == 1 ? i : j) - 1;
+    if (x >= 0 && x < (long long)out.size()) out[(size_t)x] = v;
+  }
+  std::fclose(f);
+  return out;
 }
 
 }  // namespace combblas_amd

@@ -494,6 +494,46 @@ def test_cpp_galerkin_driver():
     assert "Splitting approach is correct" in r.stdout
 
 
+def _write_triples(path, d, binary=False):
+    cols = np.repeat(d["jc"].astype(np.int64), np.diff(d["cp"]))
+    rows = d["ir"].astype(np.int64)
+    if binary:
+        rec = np.zeros(len(rows), dtype=[("r", "<i8"), ("c", "<i8"), ("v", "<f8")])
+        rec["r"], rec["c"], rec["v"] = rows, cols, d["val"]
+        with open(path, "wb") as f:
+            f.write(b"HKDT" + np.array([1, 24, 0, d["m"], d["n"], len(rows)], np.uint64).tobytes() + rec.tobytes())
+        return
+    with open(path, "w") as f:
+        f.write(f"%% written by the test\n{d['m']} {d['n']} {len(rows)}\n")
+        f.writelines(f"{r + 1} {c + 1} {float(v)!r}\n" for r, c, v in zip(rows, cols, d["val"]))
+
+
+def test_cpp_galerkin_driver_files(tmp_path):
+    """tools/galerkin with the reference's four file arguments (GalerkinNew.cpp:60-101):
+    A and the off-diagonal L as text triples, T as HKDT binary, the diagonal as a
+    vector file; ReadDistribute on the C++ mirror, then the splitting check."""
+    import os
+    import subprocess
+    from helpers import add_diag_host, load_npz, restriction_host
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(repo, "tools", "galerkin")
+    if not os.path.exists(exe):
+        pytest.skip("tools/galerkin not built (needs MPICH in /opt/conda)")
+    n = 1 << 10
+    dv = np.random.default_rng(7).uniform(0.5, 1.5, n)
+    Lh = load_npz("rmat_s10_ef16_A.npz")
+    _write_triples(tmp_path / "A.txt", add_diag_host(Lh, dv))
+    _write_triples(tmp_path / "L.txt", Lh)
+    _write_triples(tmp_path / "T.bin", restriction_host(10, 2), binary=True)
+    with open(tmp_path / "D.txt", "w") as f:
+        f.write(f"{n} 1 {n}\n")
+        f.writelines(f"{i + 1} 1 {float(v)!r}\n" for i, v in enumerate(dv))
+    r = subprocess.run([exe] + [str(tmp_path / x) for x in ("A.txt", "L.txt", "D.txt", "T.bin")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Data read" in r.stdout and "Splitting approach is correct" in r.stdout
+
+
 def _self_grid_1x1(cbg):
     class Self:
         def bcast(self, comm, arr, root):

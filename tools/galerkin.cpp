@@ -2,6 +2,8 @@
 // MI355X path, written against the C++ mirror header.  Synthetic operands: A = R-MAT
 // (off-diagonal, loops removed) plus a seeded diagonal, T = restriction operator.
 //   mpirun -n P ./galerkin <scale> [order]        (P a perfect square)
+// or the reference's file arguments (triples files read by ReadDistribute):
+//   mpirun -n P ./galerkin <Matrix> <OffDiagonal> <Diagonal> <T>
 #include <mpi.h>
 
 #include <cstdio>
@@ -18,18 +20,30 @@ int main(int argc, char* argv[]) {
   MPI_Init(&argc, &argv);
   int myrank;
   MPI_Comm_rank(MPI_COMM_WORLD, &myrank);
-  const int scale = argc > 1 ? std::atoi(argv[1]) : 16, order = argc > 2 ? std::atoi(argv[2]) : 2;
+  const bool files = argc >= 5;
+  const int scale = !files && argc > 1 ? std::atoi(argv[1]) : 16, order = !files && argc > 2 ? std::atoi(argv[2]) : 2;
   int rc = 0;
   {
     auto fullWorld = std::make_shared<CommGrid>(MPI_COMM_WORLD, 0, 0);
-    const int n = 1 << scale;
-    std::vector<double> dvec(n);
-    std::mt19937_64 rng(7);
-    std::uniform_real_distribution<double> u(0.5, 1.5);
-    for (auto& x : dvec) x = u(rng);
-    PMat L = PMat::rmat(fullWorld, scale, 16);
-    PMat A = PMat::rmat(fullWorld, scale, 16);
-    {  // A = L + D: D has this rank's diagonal entries
+    PMat A(fullWorld), L(fullWorld), T(fullWorld), S(fullWorld), SD(fullWorld);
+    std::vector<double> dvec;
+    if (files) {  // GalerkinNew.cpp:92-101
+      A.ReadDistribute(argv[1], 0);
+      L.ReadDistribute(argv[2], 0);
+      T.ReadDistribute(argv[4], 0);
+      S.ReadDistribute(argv[4], 0);
+      SD.ReadDistribute(argv[4], 0);
+      dvec = ReadDistributeVector(argv[3]);
+      if (myrank == 0) std::printf("Data read\n");
+    } else {
+      const int n = 1 << scale;
+      dvec.resize(n);
+      std::mt19937_64 rng(7);
+      std::uniform_real_distribution<double> u(0.5, 1.5);
+      for (auto& x : dvec) x = u(rng);
+      L = PMat::rmat(fullWorld, scale, 16);
+      A = PMat::rmat(fullWorld, scale, 16);
+      // A = L + D: D has this rank's diagonal entries
       const int pr = fullWorld->GetGridRows(), pc = fullWorld->GetGridCols();
       const int r = fullWorld->GetRankInProcCol(), c = fullWorld->GetRankInProcRow();
       const int mper = n / pr, nper = n / pc;
@@ -38,15 +52,15 @@ int main(int argc, char* argv[]) {
       for (int i = std::max(r0, c0); i < std::min(r1, c1); ++i) t.emplace_back(i - r0, i - c0, dvec[i]);
       PMat D(new DCCols(r1 - r0, c1 - c0, (int)t.size(), t.data(), false), fullWorld, n, n);
       A += D;
+      T = PMat::restriction(fullWorld, scale, order);
+      S = PMat::restriction(fullWorld, scale, order);
+      SD = PMat::restriction(fullWorld, scale, order);
     }
-    PMat T = PMat::restriction(fullWorld, scale, order);
-    PMat S = PMat::restriction(fullWorld, scale, order);
     S.Transpose();
     PMat AT = PSpGEMM<PTDD>(A, T);
     PMat SAT = PSpGEMM<PTDD>(S, AT);
     PMat LT = PSpGEMM<PTDD>(L, T);
     PMat SLT = PSpGEMM<PTDD>(S, LT);
-    PMat SD = PMat::restriction(fullWorld, scale, order);
     SD.Transpose();
     SD.DimApply(Column, dvec, multiplies<double>());
     PMat SDT = PSpGEMM<PTDD>(SD, T);
