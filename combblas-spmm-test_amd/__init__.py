@@ -283,6 +283,13 @@ def LocalHybridSpGEMM(A, B, sr=PlusTimesSRing, stream=None):
     return C
 
 
+def LocalSpGEMM(A, B, sr=PlusTimesSRing, stream=None):
+    """The reference's heap kernel (mtSpGEMM.h:73-202, HashSpGEMMTest.cpp:75): same C
+    structure as LocalHybridSpGEMM (rows ascending per column); the heap's summation
+    order only changes fp rounding, so the one device kernel serves both entry points."""
+    return LocalHybridSpGEMM(A, B, sr, stream)
+
+
 def last_stats():
     f, n, nb, ns = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     a, b = ctypes.c_double(), ctypes.c_double()

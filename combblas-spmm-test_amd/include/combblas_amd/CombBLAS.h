@@ -7,6 +7,7 @@
 //   SpParMat<IT,NT,DER>        SpParMat.h         SpParMat<IT,NT,DER>
 //   PlusTimesSRing/MinPlusSRing Semirings.h:212   PlusTimesSRing/MinPlusSRing
 //   LocalHybridSpGEMM          mtSpGEMM.h:212     LocalHybridSpGEMM  (returns a device SpDCCols*)
+//   LocalSpGEMM (heap)         mtSpGEMM.h:73      LocalSpGEMM (same kernel; summation order differs only)
 //   Mult_AnXBn_DoubleBuff      ParFriends.h:798   Mult_AnXBn_DoubleBuff
 //   Mult_AnXBn_Synch           ParFriends.h:1004  Mult_AnXBn_Synch
 //   PSpGEMM                    SpParMat.h:454     PSpGEMM
@@ -459,6 +460,12 @@ SpDCCols<IT, NTO>* LocalHybridSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<
   if (clearA) delete const_cast<SpDCCols<IT, NT1>*>(&A);
   if (clearB) delete const_cast<SpDCCols<IT, NT2>*>(&B);
   return new SpDCCols<IT, NTO>(c);
+}
+// LocalSpGEMM (heap kernel, mtSpGEMM.h:73-202): same C structure; the heap's
+// summation order only changes fp rounding, so it runs the same device kernel
+template <class SR, class NTO, class IT, class NT1, class NT2>
+SpDCCols<IT, NTO>* LocalSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
+  return LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
 }
 
 namespace detail {

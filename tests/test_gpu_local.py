@@ -391,6 +391,24 @@ def test_multtest_sevenvertex(cbg):
     g.destroy()
 
 
+def test_hashspgemmtest_largeseq(cbg, tmp_path):
+    """ReleaseTests/HashSpGEMMTest.cpp:66-83: read A, B and the control C, then the
+    local LocalSpGEMM(Alocal, Blocal) must equal CClocal (SpDCCols::operator==).  A and
+    B are the reference's largeseq triples files (ReadDistribute); the control is the
+    reference's own product (golden), written as Matrix Market and read back."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    g = _self_grid(cbg)
+    A = cbg.SpParMat.ReadDistribute(g, os.path.join(gold, "largeseq_input1_0.triples"))
+    B = cbg.SpParMat.ReadDistribute(g, os.path.join(gold, "largeseq_input2_0.triples"))
+    cbg.write_mm(str(tmp_path / "C.mtx"), load_npz("largeseq_C_local_plus.npz"))
+    CC = cbg.SpParMat.ParallelReadMM(g, str(tmp_path / "C.mtx"), True, "max")
+    C = cbg.LocalSpGEMM(A.tile, B.tile)
+    assert C == CC.tile
+    assert C.nnz == 29677
+    g.destroy()
+
+
 def test_cpp_multtest_driver():
     """tools/multtest (C++ mirror header; built by __graft_entry__.build()) prints the
     reference MultTest's success lines for the bundled sevenvertex inputs."""
