@@ -1641,31 +1641,43 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
 }
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
+// bit c: hash slab class c (CBG_HASH_TABLES order) runs on the side stream
+// (CBG_SIDE_HASH overrides)
+static int side_hash_classes() {
+  static const char* e = getenv("CBG_SIDE_HASH");
+  return e ? (int)strtol(e, nullptr, 0) : 0;
+}
+
 template <int SR>
 static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp, const cbg_tile& A,
-                         const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
+                         const cbg_tile& B, cbg_tile& C, hipStream_t s, hipStream_t side, DeferredFree& df) {
   const SlabRec* at[SLAB_NCLS];
   int64_t o = 0;
   for (int c = 0; c < SLAB_NCLS; ++c) {
     at[c] = list + o;
     o += ncls[c];
   }
+  // hash classes whose bit is set in side_hash_classes() queue behind the
+  // small-column bins on the side stream, so that they fill its tail while
+  // the main stream still runs the bitmap slabs
+  const int sm = side_hash_classes();
+  auto hs = [&](int c) { return (sm >> c) & 1 ? side : s; };
   launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s, df);
   launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s, df);
   static_assert(SLAB_HASH_NCLS == 9, "hash slab classes (CBG_HASH_TABLES)");
-  launch_slab_hash<SR, 512, 256>(at[2], ncls[2], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 768, 256>(at[3], ncls[3], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 1024, 256>(at[4], ncls[4], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 1536, 256>(at[5], ncls[5], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 2048, 256>(at[6], ncls[6], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 512, 256>(at[2], ncls[2], bp, A, B, C, hs(0), df);
+  launch_slab_hash<SR, 768, 256>(at[3], ncls[3], bp, A, B, C, hs(1), df);
+  launch_slab_hash<SR, 1024, 256>(at[4], ncls[4], bp, A, B, C, hs(2), df);
+  launch_slab_hash<SR, 1536, 256>(at[5], ncls[5], bp, A, B, C, hs(3), df);
+  launch_slab_hash<SR, 2048, 256>(at[6], ncls[6], bp, A, B, C, hs(4), df);
 #ifndef CBG_HBS_3072
 #define CBG_HBS_3072 512
 #define CBG_HBS_4096 512
 #endif
-  launch_slab_hash<SR, 3072, CBG_HBS_3072>(at[7], ncls[7], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 4096, CBG_HBS_4096>(at[8], ncls[8], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, s, df);
-  launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, s, df);
+  launch_slab_hash<SR, 3072, CBG_HBS_3072>(at[7], ncls[7], bp, A, B, C, hs(5), df);
+  launch_slab_hash<SR, 4096, CBG_HBS_4096>(at[8], ncls[8], bp, A, B, C, hs(6), df);
+  launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, hs(7), df);
+  launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, hs(8), df);
 }
 
 // (column, panel) pairs with fewer products re-mark their bitmap in the numeric
@@ -1816,6 +1828,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     CBG_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   }
+  // CBG_SIDE=0/1/2/3: small-column bins of the symbolic (bit 0) / numeric (bit 1)
+  // on the side stream (default 3), else serialized on the main stream
+  static const int side_bits = getenv("CBG_SIDE") ? atoi(getenv("CBG_SIDE")) : 3;
+  const hipStream_t ssym = (side_bits & 1) ? side : s, snum = (side_bits & 2) ? side : s;
   auto fork = [&](hipStream_t main) {
     CBG_HIP(hipEventRecord(ev_fork, main));
     CBG_HIP(hipStreamWaitEvent(side, ev_fork, 0));
@@ -1891,12 +1907,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   {
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
-    launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, side);
-    launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, side);
-    launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, side);
-    launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, side);
-    launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, side);
-    launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, side);
+    launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, ssym);
   }
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
@@ -2012,11 +2028,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, side, df);
-  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, side, df);
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
+  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
   if (nslabs > 0) {
-    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, df);
-    else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, df);
+    if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
+    else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);
   }
   join(s);
   // compaction of C's columns

@@ -26,6 +26,7 @@ def main():
     p.add_argument("--grid", default="1x2")
     p.add_argument("--ranks", default=None)
     p.add_argument("--reps", type=int, default=1)
+    p.add_argument("--pieces", type=int, default=1, help="multiply B's tile in this many column pieces")
     a = p.parse_args()
     pr, pc = (int(x) for x in a.grid.split("x"))
     ranks = [int(x) for x in a.ranks.split(",")] if a.ranks else list(range(pr * pc))
@@ -36,17 +37,29 @@ def main():
         r, c = rk // pc, rk % pc
         Ap = cbg.rmat_tile(a.scale, a.ef, grid=(pr, 1), pos=(r, 0))
         Bp = cbg.rmat_tile(a.scale, a.ef, grid=(1, pc), pos=(0, c))
+        pieces = []
+        rest = Bp
+        for q in range(a.pieces - 1):
+            left, rest2 = rest.split_cols(rest.n // (a.pieces - q))
+            pieces.append(left)
+            rest = rest2
+        pieces.append(rest)
         cbg.synchronize()
         best = None
         for _ in range(a.reps):
-            t0 = time.perf_counter()
-            C = cbg.LocalHybridSpGEMM(Ap, Bp)
-            cbg.synchronize()
-            dt = time.perf_counter() - t0
-            st = cbg.last_stats()
-            nnz = C.nnz
-            C.free()
-            del C
+            dt = 0.0
+            st = dict(flops=0, nnz=0, ms_symbolic=0.0, ms_numeric=0.0, n_big=0, n_slabs=0)
+            nnz = 0
+            for Bq in pieces:
+                t0 = time.perf_counter()
+                C = cbg.LocalHybridSpGEMM(Ap, Bq)
+                cbg.synchronize()
+                dt += time.perf_counter() - t0
+                for k, v in cbg.last_stats().items():
+                    st[k] += v
+                nnz += C.nnz
+                C.free()
+                del C
             best = dt if best is None else min(best, dt)
         bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * Bp.nnz + 8 * Bp.n
         ms = st["ms_symbolic"] + st["ms_numeric"]
@@ -56,6 +69,9 @@ def main():
         tot_f += st["flops"]
         tot_n += nnz
         Ap.free()
+        for Bq in pieces:
+            if Bq is not Bp:
+                Bq.free()
         Bp.free()
     g = json.load(open(os.path.join(REPO, "tests", "golden", "golden.json")))["rmat"].get(f"s{a.scale}_ef{a.ef}")
     if g and len(ranks) == pr * pc:
