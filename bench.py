@@ -247,6 +247,9 @@ def main():
 
     if rank == 0:
         traffic, traffic_src = pmc_traffic(scale, a.ef, a.phases) if N == 1 else (None, None)
+        # measured side of the roofline (north_star: "% of measured HBM bandwidth"),
+        # after the timed region: a 16-B-per-lane device copy of 4 GiB, 10 times
+        peak_measured = cbg.hbm_copy_bandwidth(4 << 30, 10)
         out = {
             "metric": "nnz(C)/sec for A·A (R-MAT scale %d) at %d GPUs" % (scale, N),
             "value": nnz_c * a.steps / dt,
@@ -271,6 +274,9 @@ def main():
                      "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "peak_measured": peak_measured, "frac_measured": achieved / peak_measured,
+                         "peak_measured_method": "16-B/lane device copy of 4 GiB x10 (read+write bytes), "
+                                                 "cbg_hbm_copy_bandwidth",
                          "traffic_source": traffic_src,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
                          "ms_avg": ms_avg, "bytes_alg": bytes_alg},

@@ -65,7 +65,7 @@ class CHostComm(ctypes.Structure):
 # every symbol include/cbg.h declares (checked by tests/test_capi.py)
 EXPORTS = [
     "cbg_version", "cbg_last_error", "cbg_set_device", "cbg_device_count", "cbg_pool_stats", "cbg_pool_trim",
-    "cbg_synchronize", "cbg_tile_upload", "cbg_tile_download", "cbg_tile_free", "cbg_tile_split_cols",
+    "cbg_synchronize", "cbg_hbm_copy_bandwidth", "cbg_tile_upload", "cbg_tile_download", "cbg_tile_free", "cbg_tile_split_cols",
     "cbg_tile_split_rows", "cbg_tile_digest", "cbg_rmat_tile", "cbg_local_spgemm", "cbg_local_symbolic", "cbg_merge",
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
@@ -101,6 +101,7 @@ def lib():
         "cbg_pool_stats": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
         "cbg_pool_trim": ([], i32),
         "cbg_synchronize": ([], i32),
+        "cbg_hbm_copy_bandwidth": ([i64, i32, ctypes.POINTER(ctypes.c_double)], i32),
         "cbg_tile_upload": ([T, T], i32),
         "cbg_tile_download": ([T, T], i32),
         "cbg_tile_free": ([T], i32),
@@ -312,6 +313,14 @@ MultiwayMerge = MergeAll  # MultiwayMerge.h:409-526: same result, threaded in th
 
 def synchronize():
     _check(lib().cbg_synchronize())
+
+
+def hbm_copy_bandwidth(nbytes=4 << 30, reps=10):
+    """Measured HBM bandwidth (GB/s) of a 16-B-per-lane device copy: the measured
+    roofline peak the bench reports beside the spec peak."""
+    g = ctypes.c_double()
+    _check(lib().cbg_hbm_copy_bandwidth(nbytes, reps, ctypes.byref(g)))
+    return g.value
 
 
 def device_count():

@@ -95,6 +95,14 @@ int cbg_pool_trim(void) {
     return CBG_OK;
   });
 }
+int cbg_hbm_copy_bandwidth(int64_t bytes, int reps, double* gbps) {
+  if (!gbps || bytes <= 0 || reps <= 0) return fail(CBG_ERR_INVALIDPARAMS, "cbg_hbm_copy_bandwidth: bad arguments");
+  return guard([&] {
+    *gbps = cbg::hbm_copy_gbps(bytes, reps);
+    return CBG_OK;
+  });
+}
+
 int cbg_synchronize(void) {
   return guard([&] {
     CBG_HIP(hipDeviceSynchronize());

@@ -138,4 +138,7 @@ void tile_dim_apply(cbg_tile& t, int dim, const double* vec_host, int op, hipStr
 void restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile& out,
                       hipStream_t s);
 
+// measured HBM bandwidth: 16-B-per-lane device copy (cbg_ops.hip)
+double hbm_copy_gbps(int64_t bytes, int reps);
+
 }  // namespace cbg

@@ -4,6 +4,8 @@
 //   tile_dim_apply     SpParMat::DimApply (SpParMat.cpp:801): x(i,j) = op(x(i,j), v[j] or v[i])
 //   restriction_tile   the restriction operator T of the multigrid driver
 //                      (mfiles/genrestrict.m: n x n/order, ~n nonzeros, values in (0,1])
+#include <algorithm>
+
 #include <hipcub/hipcub.hpp>
 
 #include "cbg_device.h"
@@ -158,6 +160,79 @@ void restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int p
     if (k == ~0ULL) hi = mid; else lo = mid + 1;
   }
   keys_to_tile(k1.p, v1.p, lo, rows, c1 - c0, out, s);
+}
+
+// ---------------------------------------------------------------- HBM copy roofline
+// The measured side of the roofline: a streaming copy, 16 B per lane, each
+// lane keeping 4 loads in flight before its stores (MI355X_MICROARCH.md:
+// 6.29 TB/s for a float4 copy).  Bytes moved = 2 x the buffer (read + write).
+__global__ __launch_bounds__(256) void k_copy16(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+// the same with nontemporal loads and stores (streamed once: keep them out of L2/MALL)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_copy16_nt(const uint4* __restrict__ src_, uint4* __restrict__ dst_,
+                                                   int64_t n) {
+  const v4u* __restrict__ src = reinterpret_cast<const v4u*>(src_);
+  v4u* __restrict__ dst = reinterpret_cast<v4u*>(dst_);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const v4u a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride),
+              c = __builtin_nontemporal_load(src + i + 2 * stride),
+              d = __builtin_nontemporal_load(src + i + 3 * stride);
+    __builtin_nontemporal_store(a, dst + i);
+    __builtin_nontemporal_store(b, dst + i + stride);
+    __builtin_nontemporal_store(c, dst + i + 2 * stride);
+    __builtin_nontemporal_store(d, dst + i + 3 * stride);
+  }
+  for (; i < n; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+double hbm_copy_gbps(int64_t bytes, int reps) {
+  const int64_t n = std::max<int64_t>(bytes / 16, 1);
+  uint4 *a = nullptr, *b = nullptr;
+  CBG_HIP(hipMalloc(&a, n * 16));
+  CBG_HIP(hipMalloc(&b, n * 16));
+  CBG_HIP(hipMemset(a, 1, n * 16));
+  CBG_HIP(hipMemset(b, 0, n * 16));
+  int dev = 0, cus = 256;
+  CBG_HIP(hipGetDevice(&dev));
+  CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  static const char* eg = getenv("CBG_COPY_BLOCKS_PER_CU");  // tuning knob
+  const int grid = cus * (eg ? atoi(eg) : 128);  // 8: 4.7, 32: 5.0, 128: 5.3-5.5 TB/s (nt)
+  hipEvent_t e0, e1;
+  CBG_HIP(hipEventCreate(&e0));
+  CBG_HIP(hipEventCreate(&e1));
+  hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, nullptr, a, b, n);  // warm-up
+  CBG_HIP(hipEventRecord(e0, nullptr));
+  static const char* em = getenv("CBG_COPY_NT");
+  const bool nt = !em || atoi(em) != 0;
+  for (int r = 0; r < reps; ++r) {
+    if (nt)
+      hipLaunchKernelGGL(k_copy16_nt, dim3(grid), dim3(256), 0, nullptr, (r & 1) ? b : a, (r & 1) ? a : b, n);
+    else
+      hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, nullptr, (r & 1) ? b : a, (r & 1) ? a : b, n);
+  }
+  CBG_HIP(hipEventRecord(e1, nullptr));
+  CBG_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CBG_HIP(hipEventElapsedTime(&ms, e0, e1));
+  CBG_HIP(hipEventDestroy(e0));
+  CBG_HIP(hipEventDestroy(e1));
+  CBG_HIP(hipFree(a));
+  CBG_HIP(hipFree(b));
+  return 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;
 }
 
 }  // namespace cbg

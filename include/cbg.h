@@ -76,6 +76,9 @@ int cbg_device_count(int* count);
 int cbg_pool_stats(size_t* in_use, size_t* cached);
 int cbg_pool_trim(void);
 int cbg_synchronize(void);
+/* measured side of the HBM roofline (no reference counterpart): a 16-byte-per-lane
+ * device copy of `bytes` run `reps` times; *gbps = 2 * bytes * reps / time (GB/s) */
+int cbg_hbm_copy_bandwidth(int64_t bytes, int reps, double* gbps);
 
 /* ---------------- tiles ---------------- */
 /* host -> device copy (arrays of *dst are allocated by libcbg) */

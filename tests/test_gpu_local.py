@@ -658,3 +658,9 @@ def test_phased_scale22_vs_oracle(cbg):
     grid.destroy()
     assert (nnz, hs, hv) == (g["nnz"], g["hs"], g["hv"])
     assert nnz == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"]
+
+
+def test_hbm_copy_bandwidth(cbg):
+    """The measured roofline peak the bench reports: a plausible HBM3E copy rate."""
+    g = cbg.hbm_copy_bandwidth(1 << 30, 5)
+    assert 1000.0 < g < 8000.0
