@@ -136,6 +136,17 @@ struct RowVal {
   double v;
 };
 
+// claim `row` in an LDS hash of mask + 1 slots (linear probing from h):
+// 1 if this call inserted it, 0 if it was there
+__device__ __forceinline__ int hash_claim(int* keys, unsigned h, unsigned mask, int row) {
+  while (true) {
+    const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+    if (old == EMPTY_KEY) return 1;
+    if (old == row) return 0;
+    h = (h + 1) & mask;
+  }
+}
+
 // insert-or-accumulate into an LDS hash table (linear probing)
 template <int SR, int LOGT>
 __device__ __forceinline__ void hash_acc(int* keys, double* vals, int row, double v) {
@@ -213,13 +224,7 @@ __global__ __launch_bounds__(256) void k_sym_wave(const int32_t* __restrict__ pe
         pref, WAVE, 0, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
         [&](const SegI& g, int u) { return irA[g.off + u]; },
         [&](int row) {
-          unsigned h = hash_slot<LOGT>(row);
-          while (true) {
-            const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-            if (old == EMPTY_KEY) { ++count; break; }
-            if (old == row) break;
-            h = (h + 1) & (T - 1);
-          }
+          count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row);
         });
     wave_sync();
   }
@@ -270,13 +275,7 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
         pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
         [&](const SegI& g, int u) { return irA[g.off + u]; },
         [&](int row) {
-          unsigned h = hash_slot<LOGT>(row);
-          while (true) {
-            const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-            if (old == EMPTY_KEY) { ++count; break; }
-            if (old == row) break;
-            h = (h + 1) & (T - 1);
-          }
+          count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row);
         });
     __syncthreads();
   }
@@ -483,13 +482,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
           pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
           [&](const SegI& g, int u) { return irA[g.off + u]; },
           [&](int row) {
-            unsigned h = ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1);
-            while (true) {
-              const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-              if (old == EMPTY_KEY) { ++count; break; }
-              if (old == row) break;
-              h = (h + 1) & (unsigned)(T - 1);
-            }
+            count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
           });
       hook(2);
       count = wave_sum(count);
@@ -676,13 +669,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
       pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
       [&](const SegI& g, int u) { return irA[g.off + u]; },
       [&](int row) {
-        unsigned h = ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1);
-        while (true) {
-          const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-          if (old == EMPTY_KEY) { ++count; break; }
-          if (old == row) break;
-          h = (h + 1) & (unsigned)(T - 1);
-        }
+        count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
       });
   hook(2);
   count = wave_sum(count);
