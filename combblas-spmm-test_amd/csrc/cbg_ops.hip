@@ -206,30 +206,35 @@ double hbm_copy_gbps(int64_t bytes, int reps) {
   CBG_HIP(hipMalloc(&b, n * 16));
   CBG_HIP(hipMemset(a, 1, n * 16));
   CBG_HIP(hipMemset(b, 0, n * 16));
+  CBG_HIP(hipDeviceSynchronize());
   int dev = 0, cus = 256;
   CBG_HIP(hipGetDevice(&dev));
   CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   static const char* eg = getenv("CBG_COPY_BLOCKS_PER_CU");  // tuning knob
   const int grid = cus * (eg ? atoi(eg) : 128);  // 8: 4.7, 32: 5.0, 128: 5.3-5.5 TB/s (nt)
+  static const char* em = getenv("CBG_COPY_NT");
+  const bool nt = !em || atoi(em) != 0;
+  hipStream_t st = nullptr;
+  CBG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  auto launch = [&](const uint4* src, uint4* dst) {
+    if (nt)
+      hipLaunchKernelGGL(k_copy16_nt, dim3(grid), dim3(256), 0, st, src, dst, n);
+    else
+      hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, st, src, dst, n);
+  };
   hipEvent_t e0, e1;
   CBG_HIP(hipEventCreate(&e0));
   CBG_HIP(hipEventCreate(&e1));
-  hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, nullptr, a, b, n);  // warm-up
-  CBG_HIP(hipEventRecord(e0, nullptr));
-  static const char* em = getenv("CBG_COPY_NT");
-  const bool nt = !em || atoi(em) != 0;
-  for (int r = 0; r < reps; ++r) {
-    if (nt)
-      hipLaunchKernelGGL(k_copy16_nt, dim3(grid), dim3(256), 0, nullptr, (r & 1) ? b : a, (r & 1) ? a : b, n);
-    else
-      hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, nullptr, (r & 1) ? b : a, (r & 1) ? a : b, n);
-  }
-  CBG_HIP(hipEventRecord(e1, nullptr));
+  launch(a, b);  // warm-up
+  CBG_HIP(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) launch((r & 1) ? b : a, (r & 1) ? a : b);
+  CBG_HIP(hipEventRecord(e1, st));
   CBG_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
   CBG_HIP(hipEventElapsedTime(&ms, e0, e1));
   CBG_HIP(hipEventDestroy(e0));
   CBG_HIP(hipEventDestroy(e1));
+  CBG_HIP(hipStreamDestroy(st));
   CBG_HIP(hipFree(a));
   CBG_HIP(hipFree(b));
   return 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timeline of one local multiply from a rocprofv3 kernel_trace.csv (the LAST multiply:
-dispatches after the last k_colmap launch): per kernel start/end offsets, stream, and
+dispatches from the last k_colmap launch to the last k_col_scatter): per kernel start/end offsets, stream, and
 the busy union / gaps.  usage: tools/timeline.py k_kernel_trace.csv"""
 import csv
 import sys
@@ -9,6 +9,9 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("cbg::k_colmap(")]
 rows = rows[starts[-1]:]
+ends = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("cbg::k_col_scatter(")]
+if ends:  # the multiply ends with its column scatter (later dispatches: e.g. the bench's copy-rate probe)
+    rows = rows[:ends[-1] + 1]
 t0 = int(rows[0]["Start_Timestamp"])
 busy = []
 for r in rows:
