@@ -305,12 +305,16 @@ __device__ __forceinline__ void bitonic_sort_kv(int* keys, double* vals, int tid
 // and each entry's position inside its bucket is its rank among the few
 // entries of that bucket.  O(T + n * bucket size) work, 3 barriers.
 // Scratch: boff[NB+1], cur[NB] ints, members[n] (slot ids).
-template <int T, int BS, int NB>
+template <int T, int BS, int NB, bool MOFF = false>
 __device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* vals, int lo, int bshift, int* boff,
                                                  int* cur, unsigned short* members, int* tmp,
                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val,
-                                                 int64_t obase) {
+                                                 int64_t obase, unsigned short* moff = nullptr) {
+  // MOFF: pass 2 also stores each entry's row offset inside its bucket
+  // ((key - lo) mod 2^bshift, < 2^16), so the rank loop reads one u16 per
+  // bucket member instead of a slot id and then that slot's key
   const int tid = threadIdx.x;
+  const int omask = (1 << bshift) - 1;
   for (int b = tid; b < NB; b += BS) cur[b] = 0;
   __syncthreads();
   for (int j = tid; j < T; j += BS) {
@@ -330,7 +334,11 @@ __device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* 
   __syncthreads();
   for (int j = tid; j < T; j += BS) {
     const int k = keys[j];
-    if (k != EMPTY_KEY) members[atomicAdd(&cur[(k - lo) >> bshift], 1)] = (unsigned short)j;
+    if (k != EMPTY_KEY) {
+      const int pos = atomicAdd(&cur[(k - lo) >> bshift], 1);
+      members[pos] = (unsigned short)j;
+      if (MOFF) moff[pos] = (unsigned short)((k - lo) & omask);
+    }
   }
   __syncthreads();
   for (int p = tid; p < total; p += BS) {
@@ -339,7 +347,12 @@ __device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* 
     const int b = (k - lo) >> bshift;
     int r = boff[b];
     const int e = boff[b + 1];
-    for (int q = boff[b]; q < e; ++q) r += keys[members[q]] < k;
+    if (MOFF) {
+      const int mo = (k - lo) & omask;
+      for (int q = boff[b]; q < e; ++q) r += (int)moff[q] < mo;
+    } else {
+      for (int q = boff[b]; q < e; ++q) r += keys[members[q]] < k;
+    }
     out_ir[obase + r] = k;
     out_val[obase + r] = vals[j];
   }

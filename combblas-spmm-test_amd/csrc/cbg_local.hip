@@ -1291,6 +1291,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 // numeric of a sparse (column, panel) pair (hash-mode slab, <= SPARSE_SLAB_MAX
 // products): LDS hash sized to the pair's nnz, sorted emit by row buckets
+#ifndef CBG_EMIT_MOFF  // emit ranks from cached in-bucket row offsets (1 LDS read per bucket member)
+#define CBG_EMIT_MOFF 1
+#endif
 #ifndef CBG_EMIT_NB_DIV  // emit buckets of a hash slab: power of two <= T / DIV
 #define CBG_EMIT_NB_DIV 4
 #endif
@@ -1300,9 +1303,11 @@ struct SlabHashLds {
   static constexpr int LOGNB = 31 - __builtin_clz(T / CBG_EMIT_NB_DIV);
   static constexpr int NB = 1 << LOGNB;  // row buckets of the sorted emit (power of two <= T/4)
   static constexpr int MEMB = (T * CBG_HASH_LOAD_DEN + CBG_HASH_LOAD_NUM - 1) / CBG_HASH_LOAD_NUM;  // max nnz
-  // vals[T] f64 | bv[BS] f64 | keys[T] | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
+  // vals[T] f64 | keys[T] | bv[BS] f64 | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
                                (2 * NB + 4) * 4 + MEMB * 2;
+  // the emit's in-bucket row offsets (u16) reuse bv|pref|st, idle during the emit
+  static constexpr bool MOFF_FITS = MEMB * 2 <= BS * 8 + (BS + 4) * 4 + BS * 4;
 };
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
@@ -1326,9 +1331,9 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   static_assert(PF <= 2, "prefetch chunks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* vals = reinterpret_cast<double*>(smem);
-  double* bv = vals + T;
-  int* keys = reinterpret_cast<int*>(bv + BS);
-  int* pref = keys + T;
+  int* keys = reinterpret_cast<int*>(vals + T);
+  double* bv = reinterpret_cast<double*>(keys + T);  // T even: 8-B aligned
+  int* pref = reinterpret_cast<int*>(bv + BS);
   int* st = pref + BS + 4;
   int* tmp = st + BS;
   int* boff = tmp + BS / WAVE + 4;
@@ -1422,7 +1427,15 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
     if (!CMLEN)
       while ((1LL << sl) < (int64_t)(rec.hi - rec.lo)) ++sl;
     const int bshift = sl > LOGNB ? sl - LOGNB : 0;
-    hash_emit_sorted<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val, rec.obase);
+    // in-bucket offsets fit u16 for panel-group slabs (span <= 2^(plog+4) rows,
+    // bshift <= 15); whole-column bins (CMLEN) use them while bshift <= 16
+    constexpr bool MOFF = L::MOFF_FITS && CBG_EMIT_MOFF;
+    if (MOFF && (!CMLEN || bshift <= 16))
+      hash_emit_sorted<T, BS, NB, MOFF>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val,
+                                        rec.obase, reinterpret_cast<unsigned short*>(bv));
+    else
+      hash_emit_sorted<T, BS, NB, false>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val,
+                                         rec.obase);
     __syncthreads();  // LDS is reset for the next slab
     phase_mark(tmark, 15);
     if (!has_next) break;
