@@ -149,8 +149,15 @@ def main():
         with open(os.path.join(HERE, "golden.json"), "w") as f:
             json.dump(gold, f, indent=1, sort_keys=True)
 
-    # ---- large scales: inputs + symbolic totals only (C does not fit this host) ----
-    big = [tuple(int(x) for x in s.split("x")) for s in os.environ.get("GOLD_BIG", "20x16,20x8,22x16,22x8").split(",") if s]
+    big_scales(gold, tmp, os.environ.get("GOLD_BIG", "20x16,20x8,22x16,22x8"))
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(gold, f, indent=1, sort_keys=True)
+    multtest_fixture()
+
+
+def big_scales(gold, tmp, spec):
+    """large scales: inputs + symbolic totals only (C does not fit this host)"""
+    big = [tuple(int(x) for x in s.split("x")) for s in spec.split(",") if s]
     for scale, ef in big:
         key = f"s{scale}_ef{ef}"
         entry = {}
@@ -164,10 +171,6 @@ def main():
         print(key, "done", flush=True)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
             json.dump(gold, f, indent=1, sort_keys=True)
-
-    with open(os.path.join(HERE, "golden.json"), "w") as f:
-        json.dump(gold, f, indent=1, sort_keys=True)
-    multtest_fixture()
 
 
 def multtest_fixture():
@@ -186,6 +189,12 @@ def multtest_fixture():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "big":
+        # add large-scale symbolic totals to the existing golden.json, e.g. `big 24x16`
+        with open(os.path.join(HERE, "golden.json")) as f:
+            g = json.load(f)
+        big_scales(g, tempfile.mkdtemp(prefix="cbg_golden_"), sys.argv[2])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "multtest":
         multtest_fixture()
     else:
