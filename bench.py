@@ -38,9 +38,12 @@ def load_cbg():
     return mod
 
 
-# row-heavy grids: fewer row panels per rank tile (measured: 2x1 7 % and 4x2 2 % faster than 1x2 / 2x4)
+# row-heavy grids: fewer row panels per rank tile, and the A block row (gathered
+# before the first piece, exposed) spans fewer ranks than the B block column
+# (broadcast piece by piece behind the multiply); measured per rank tile on one
+# GPU: 2x1 7 % and 4x2 2-13 % faster than 1x2 / 2x4.  --grid RxC overrides.
 GRIDS = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2), 9: (3, 3), 16: (4, 4)}
-ROUND = "r01"
+ROUND = "r02"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -59,38 +62,69 @@ def parse():
                         "(for C larger than HBM, e.g. scale 22 on one GPU)")
     p.add_argument("--phase-consumer", choices=["none", "digest"], default="none",
                    help="what the phase callback does with each phase's device C tile")
+    p.add_argument("--grid", default=None, help="RxC process grid (default: GRIDS[N])")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--cpu-scale", type=int, default=None, help="scale of the CPU-baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=0, help="default: the CPUs this job may use")
+    p.add_argument("--cpu-scale", type=int, default=20, help="scale of the CPU-baseline sample (reference Synch)")
     return p.parse_args()
+
+
+def host_cores():
+    """CPUs this job may use: the affinity mask capped by the cgroup CPU quota (the
+    GPU box gives one GPU's job 16 of the host's cores), plus the host's lscpu shape."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) // int(per)
+    except (OSError, ValueError):
+        pass
+    shape = {}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core"):
+                shape[k.strip()] = v.strip()
+    except (OSError, ValueError):
+        pass
+    cores = min(n, quota) if quota else n
+    return max(cores, 1), dict(affinity=n, cgroup_quota=quota, **shape)
 
 
 def pmc_traffic(scale, ef, phases):
     """HBM bytes of one local multiply (all phases) at this configuration from the
     committed PMC passes (profiles/<round>_traffic_s<scale>.json, made by
     tools/profile_round.sh + tools/traffic.py: FETCH_SIZE calibrated on k_digest,
-    + WRITE_SIZE), or None."""
-    path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (ROUND, scale))
-    if not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        d = json.load(f)
-    if d.get("scale") != scale or d.get("ef") != ef or d.get("phases", 1) != phases:
-        return None, None
-    return d["traffic_bytes"], os.path.relpath(path, REPO)
+    + WRITE_SIZE), this round's file first, or None."""
+    for rnd in (ROUND, "r01"):
+        path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (rnd, scale))
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("scale") != scale or d.get("ef") != ef or d.get("phases", 1) != phases:
+            continue
+        return d["traffic_bytes"], os.path.relpath(path, REPO)
+    return None, None
 
 
 REF_DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
 
 
-def cpu_baseline_reference(scale, ef, threads):
+def cpu_baseline_reference(scale, ef, threads, algos=("synch",)):
     """The reference itself (oracle/_ref/ref_driver: our driver linked against the
     reference's CombBLAS sources, built by __graft_entry__.build() where the
     reference exists; the binary travels with the tree) timed on host cores:
     GenGraph500Data + RemoveLoops (GenWriteMatrix.cpp:101-114), then
-    Mult_AnXBn_Synch and Mult_AnXBn_DoubleBuff at 1x1 with `threads` OpenMP
-    threads, multiply time only (MPI_Wtime around the call); the better of the
-    two is reported.  None if the binary is absent or fails."""
+    Mult_AnXBn_<algo> at 1x1 with `threads` OpenMP threads, multiply time only
+    (MPI_Wtime around the call); the best of `algos` is reported.
+    Synch only by default: at scale 18 it is 2.5x faster than DoubleBuff
+    (5.9 s vs 15.6 s, whose serial MergeAll dominates), so it is the better-of.
+    None if the binary is absent or fails."""
     import subprocess
     import tempfile
     if not os.path.exists(REF_DRIVER):
@@ -99,13 +133,13 @@ def cpu_baseline_reference(scale, ef, threads):
     with tempfile.TemporaryDirectory() as d:
         a = os.path.join(d, "A.cbgt")
         r = subprocess.run([REF_DRIVER, "gen", str(scale), str(ef), a], capture_output=True, text=True, env=env,
-                           timeout=300)
+                           timeout=600)
         if r.returncode != 0:
             return None
         best = None
-        for algo in ("synch", "doublebuff"):
+        for algo in algos:
             r = subprocess.run([REF_DRIVER, "mult", algo, "plus", a, a, "-"], capture_output=True, text=True,
-                               env=env, timeout=600)
+                               env=env, timeout=900)
             if r.returncode != 0:
                 return None
             nnz = dt = None
@@ -121,6 +155,19 @@ def cpu_baseline_reference(scale, ef, threads):
             if best is None or nnz / dt > best[0]:
                 best = (nnz / dt, algo, dt, nnz)
     return best
+
+
+def cpu_baseline_s22():
+    """The one-off reference run at the metric's own scale (profiles/<round>_cpu_reference_s22.json,
+    tools/cpu_reference_s22.sh on the GPU box: Mult_AnXBn_Synch per B-column phase)."""
+    for rnd in (ROUND, "r01"):
+        path = os.path.join(REPO, "profiles", "%s_cpu_reference_s22.json" % rnd)
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            d["source"] = os.path.relpath(path, REPO)
+            return d
+    return None
 
 
 def cpu_baseline(scale, ef, seed, threads):
@@ -155,10 +202,19 @@ def main():
     N = max(world, 1)
     scale = a.scale if a.scale is not None else 22
     if a.phases is None:
-        a.phases = 4 if (N == 1 and scale >= 21) else 1
+        # C streamed per B-column phase where a rank's C tile does not fit its
+        # HBM: scale 22 on one GPU (297 GB), scale 24 on 8 (about 275 GB per rank)
+        a.phases = 4 if (N == 1 and scale >= 21) or scale >= 24 else 1
+    stream_c = a.phases > 1
     cbg = load_cbg()  # libcbg first: its HIP/RCCL runtimes are the ones the process uses
     cbg.lib().cbg_set_device(local_rank % max(1, cbg.device_count()))
 
+    if a.grid:
+        pr, pc = (int(x) for x in a.grid.lower().split("x"))
+    else:
+        pr, pc = GRIDS[N]
+    if pr * pc != N:
+        raise SystemExit(f"grid {pr}x{pc} does not have {N} ranks")
     if N == 1:
         class Self:
             def bcast(self, comm, arr, root):
@@ -173,7 +229,6 @@ def main():
         # Host rendezvous for the RCCL unique id over plain TCP (MASTER_PORT+1):
         # the GPU processes never import torch, whose ROCm wheel would load a
         # second HIP runtime into the process.
-        pr, pc = GRIDS[N]
         hc = cbg.TcpHostComm(rank, N, pr, pc, os.environ.get("MASTER_ADDR", "127.0.0.1"),
                              int(os.environ.get("MASTER_PORT", "29500")) + 1)
         uid = hc.bcast_object(cbg.CommGrid.unique_id() if rank == 0 else None, root=0)
@@ -202,7 +257,7 @@ def main():
 
     def step():
         """one complete multiply; returns (local nnz(C), resident C or None)"""
-        if a.phases <= 1:
+        if not stream_c:
             C = mult(A, B, exec_mode=exec_mode)
             return C.tile.nnz, C
         seen = [0]
@@ -221,82 +276,111 @@ def main():
         if C is not None:
             C.tile.free()
             C = None
+    # the measured side of the roofline, before the timed region (and again after)
+    peaks = [cbg.hbm_copy_bandwidth(4 << 30, 10) for _ in range(2)] if rank == 0 else []
+    # K steps, each bracketed by barrier + synchronize and timed as the max over
+    # ranks; the whole loop is bracketed the same way (the driver contract)
+    ms_local, step_s = [], []
     grid.barrier()
     cbg.synchronize()
-    ms_local = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if C is not None:
             C.tile.free()
+        grid.barrier()
+        ts = time.perf_counter()
         nnz_local, C = step()
+        cbg.synchronize()
+        te = time.perf_counter()
         st = cbg.last_stats()
         ms_local.append(st["ms_symbolic"] + st["ms_numeric"])
+        step_s.append(te - ts)
     cbg.synchronize()
     grid.barrier()
     dt = time.perf_counter() - t0
     dt = grid.allreduce_max(dt)
+    step_s = [grid.allreduce_max(x) for x in step_s]
+    med = sorted(step_s)[len(step_s) // 2] if len(step_s) % 2 else \
+        0.5 * (sorted(step_s)[len(step_s) // 2 - 1] + sorted(step_s)[len(step_s) // 2])
     nnz_c = grid.allreduce_sum(nnz_local)
     st = cbg.last_stats()
     flops = grid.allreduce_sum(st["flops"])
-    # algorithmic bytes of the local multiply: 16F + 12 nnz(C) + 32 nnz(B) + 8 n
-    nnz_b = B.tile.nnz
-    bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * nnz_b + 8 * B.tile.n
+    # algorithmic bytes of this rank's local multiply:
+    # 16F + 12 nnz(C) + 32 nnz(B) + 8 n, B = the rank's B block column
+    col_nnz = [grid.allreduce_sum(B.tile.nnz if grid.pcol == c else 0) for c in range(pc)]
+    bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * col_nnz[grid.pcol] + 8 * B.tile.n
     ms_avg = sum(ms_local) / len(ms_local)
     achieved = bytes_alg / (ms_avg * 1e-3) / 1e9
     achieved = grid.allreduce_max(achieved) if N > 1 else achieved
 
     if rank == 0:
         traffic, traffic_src = pmc_traffic(scale, a.ef, a.phases) if N == 1 else (None, None)
-        # measured side of the roofline (north_star: "% of measured HBM bandwidth"),
-        # after the timed region: a 16-B-per-lane device copy of 4 GiB, 10 times
-        peak_measured = cbg.hbm_copy_bandwidth(4 << 30, 10)
+        peaks += [cbg.hbm_copy_bandwidth(4 << 30, 10) for _ in range(2)]
+        peak_measured = max(peaks)
         out = {
             "metric": "nnz(C)/sec for A·A (R-MAT scale %d) at %d GPUs" % (scale, N),
-            "value": nnz_c * a.steps / dt,
+            "value": nnz_c / med,
             "unit": "nnz(C)/s",
             "n_gpus": N,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": dt / a.steps * 1e3,
+            "ms_per_step": med * 1e3,
             "higher_is_better": True,
             # every N multiplies the same scale-22 problem (total work fixed)
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic Graph500 R-MAT (SEED 0xDECAFBAD), generated on device",
+            "timing": {"value_from": "median over the steps of (barrier; step; synchronize) max over ranks "
+                                     "(BASELINE.md: median of >= 5)",
+                       "step_ms": [round(x * 1e3, 3) for x in step_s],
+                       "loop_ms_per_step": dt / a.steps * 1e3, "value_loop_mean": nnz_c * a.steps / dt},
             "config": {"workload": "R-MAT scale-%d ef%d A·A, Mult_AnXBn_%s, %s" % (
                 scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
                 "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport,
                 "phases": a.phases,
-                "C": "resident in HBM" if a.phases <= 1 else
-                     "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer},
+                "C": "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer if stream_c
+                     else "resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "peak_measured": peak_measured, "frac_measured": achieved / peak_measured,
                          "peak_measured_method": "16-B/lane device copy of 4 GiB x10 (read+write bytes), "
-                                                 "cbg_hbm_copy_bandwidth",
+                                                 "cbg_hbm_copy_bandwidth, best of 2 before and 2 after the "
+                                                 "timed region",
+                         "peak_measured_runs": peaks,
                          "traffic_source": traffic_src,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
                          "ms_avg": ms_avg, "bytes_alg": bytes_alg},
         }
         if N == 1 and not a.no_cpu_baseline:
-            threads = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-            threads = min(threads, 16)
-            cs = a.cpu_scale if a.cpu_scale is not None else min(scale, 18)
+            cores, host = host_cores()
+            threads = a.cpu_threads or cores
+            cs = a.cpu_scale
             ref = cpu_baseline_reference(cs, a.ef, threads) if a.seed == 0xDECAFBAD else None
             if ref is not None:
-                r, algo, cdt, cnnz = ref
+                r, algo_, cdt, cnnz = ref
                 out["cpu_baseline"] = {"value": r, "unit": "nnz(C)/s", "cores": threads, "kind": "reference",
                                        "sample": "R-MAT scale-%d ef%d A*A, the reference's Mult_AnXBn_%s 1x1 "
-                                                 "(oracle/_ref/ref_driver, better of Synch/DoubleBuff), %.1f s" % (
-                                                     cs, a.ef, algo.capitalize(), cdt)}
+                                                 "(oracle/_ref/ref_driver), %.1f s on %d threads" % (
+                                                     cs, a.ef, algo_.capitalize(), cdt, threads),
+                                       "host": host}
+                # cross-check at scale 18: the reference vs our restatement on the same cores
+                rr = cpu_baseline_reference(18, a.ef, threads)
+                pr_ = cpu_baseline(18, a.ef, a.seed, threads)
+                if rr and pr_:
+                    out["cpu_baseline"]["crosscheck_s18"] = {"reference_synch": rr[0],
+                                                             "port_best": pr_[0], "port_algo": pr_[1]}
             else:
-                r, algo, cdt, cnnz = cpu_baseline(cs, a.ef, a.seed, threads)
+                r, algo_, cdt, cnnz = cpu_baseline(cs, a.ef, a.seed, threads)
                 out["cpu_baseline"] = {"value": r, "unit": "nnz(C)/s", "cores": threads, "kind": "port",
                                        "sample": "R-MAT scale-%d ef%d A*A, oracle Mult_AnXBn_%s 1x1, %.1f s" % (
-                                           cs, a.ef, algo.capitalize(), cdt)}
+                                           cs, a.ef, algo_.capitalize(), cdt), "host": host}
+            s22 = cpu_baseline_s22()
+            if s22 is not None and scale == 22:
+                out["cpu_baseline_s22"] = s22
+                out["cpu_baseline_s22"]["gpu_over_cpu"] = out["value"] / s22["value"]
         print(json.dumps(out), flush=True)
     if C is not None:
         C.tile.free()

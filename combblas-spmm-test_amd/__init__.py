@@ -70,7 +70,7 @@ EXPORTS = [
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
-    "cbg_grid_transpose", "cbg_grid_block_extract",
+    "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -108,7 +108,7 @@ def lib():
         "cbg_tile_split_cols": ([T, i64, T, T], i32),
         "cbg_tile_split_rows": ([T, i64, T, T], i32),
         "cbg_tile_digest": ([T, i64, i64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
-                             ctypes.POINTER(ctypes.c_double)], i32),
+                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)], i32),
         "cbg_rmat_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
         "cbg_local_spgemm": ([T, T, i32, T, vp], i32),
         "cbg_local_symbolic": ([T, T, ctypes.POINTER(i64), ctypes.POINTER(i64), vp], i32),
@@ -131,6 +131,8 @@ def lib():
         "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
         "cbg_grid_transpose": ([vp, T, T], i32),
         "cbg_grid_block_extract": ([vp, T, i64, i64, i32, i64, i64, T], i32),
+        "cbg_grid_agree": ([vp, i32, ctypes.POINTER(i32)], i32),
+        "cbg_merge_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -190,11 +192,14 @@ class Tile:
         return dict(m=int(c.m), n=int(c.n), cp=cp, jc=jc[:c.nzc], ir=ir[:c.nnz], val=val[:c.nnz])
 
     def digest(self, roff=0, coff=0):
-        hs, hv, vs = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+        """nnz, nzc, order-free hashes hs/hv, vsum, and `unsorted`: the number of DCSC
+        order violations (rows not strictly ascending in a column, columns not
+        ascending, empty columns; 0 for a valid tile, as the reference driver counts)."""
+        hs, hv, vs, un = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double(), ctypes.c_uint64()
         _check(lib().cbg_tile_digest(ctypes.byref(self.c), roff, coff, ctypes.byref(hs), ctypes.byref(hv),
-                                     ctypes.byref(vs)))
+                                     ctypes.byref(vs), ctypes.byref(un)))
         return dict(nnz=int(self.c.nnz), nzc=int(self.c.nzc), hs="%016x" % hs.value, hv="%016x" % hv.value,
-                    vsum=vs.value)
+                    vsum=vs.value, unsorted=int(un.value))
 
     def equal(self, other, epsilon=EPSILON):
         """SpDCCols::operator== (SpDCCols.h:74-81): exact structure, ErrorTolerantEqual values."""
@@ -298,6 +303,13 @@ def last_stats():
                          ctypes.byref(ns))
     return dict(flops=f.value, nnz=n.value, ms_symbolic=a.value, ms_numeric=b.value, n_big=nb.value,
                 n_slabs=ns.value)
+
+
+def merge_stats():
+    """the last call's multiway merges: partial entries in, merged entries out, device ms."""
+    a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+    lib().cbg_merge_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return dict(entries_in=a.value, entries_out=b.value, ms=c.value)
 
 
 def MergeAll(parts, sr=PlusTimesSRing):
@@ -418,6 +430,12 @@ class CommGrid:
         v = ctypes.c_int64(int(x))
         _check(lib().cbg_grid_allreduce_sum_i64(self.h, ctypes.byref(v)))
         return v.value
+
+    def agree(self, local_rc):
+        """collective error agreement: the maximum of the ranks' codes (0 = every rank succeeded)."""
+        out = ctypes.c_int()
+        _check(lib().cbg_grid_agree(self.h, int(local_rc), ctypes.byref(out)))
+        return out.value
 
     def destroy(self):
         if self.h:

@@ -9,7 +9,7 @@ struct cbg_grid;
 namespace cbg {
 void rmat_tile(int scale, int ef, uint64_t userseed, int pr, int pc, int prow, int pcol, cbg_tile& out, hipStream_t s);
 void tile_digest(const cbg_tile& t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum,
-                 hipStream_t s);
+                 uint64_t* unsorted, hipStream_t s);
 bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s);
 int grid_shape(int nranks, int& rows, int& cols);
 cbg_grid* grid_create_rccl(int rank, int nranks, int rows, int cols, const void* uid);
@@ -23,6 +23,8 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                         int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C);
 int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out);
+int agree(cbg_grid* g, int rc);
+std::string& step_error();
 int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, int dim, int64_t lo, int64_t hi,
                        cbg_tile& out);
 }  // namespace cbg
@@ -177,10 +179,12 @@ int cbg_tile_split_rows(const cbg_tile* t, int64_t cut, cbg_tile* top, cbg_tile*
   });
 }
 
-int cbg_tile_digest(const cbg_tile* t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum) {
+int cbg_tile_digest(const cbg_tile* t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum,
+                    uint64_t* unsorted) {
   if (int rc = check_tile(t, true, "tile")) return rc;
+  if (!hs || !hv || !vsum) return fail(CBG_ERR_INVALIDPARAMS, "digest outputs missing");
   return guard([&] {
-    cbg::tile_digest(*t, roff, coff, hs, hv, vsum, default_stream());
+    cbg::tile_digest(*t, roff, coff, hs, hv, vsum, unsorted, default_stream());
     return CBG_OK;
   });
 }
@@ -294,6 +298,7 @@ int cbg_merge(const cbg_tile* parts, int nparts, int sr, cbg_tile* C, void* stre
   }
   return guard([&] {
     cbg::thread_stats() = cbg::LocalStats{};
+    cbg::merge_stats() = cbg::MergeStats{};
     std::vector<cbg_tile> v(parts, parts + nparts);
     cbg::merge_tiles(v, parts[0].m, parts[0].n, sr, *C, as_stream(stream));
     return CBG_OK;
@@ -364,23 +369,45 @@ int cbg_grid_allreduce_sum_i64(cbg_grid* g, int64_t* v) {
   });
 }
 
+// Collective entry points: a check that fails on some ranks only is agreed on
+// over the grid before returning, so every rank returns the code (the
+// reference MPI_Aborts every rank, SpDefs.h:69-76).
+static const char* summa_msg(int rc) {
+  return rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"
+         : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
+         : rc == CBG_ERR_NOTSQUARE   ? "needs a square grid"
+         : rc == CBG_ERR_INVALIDPARAMS
+             ? "bad parameters (a B tile with fewer columns than phases, or a phase callback failed)"
+         : rc == CBG_ERR_OOM ? "device memory exhausted on a rank of the grid"
+         : rc == CBG_ERR_RCCL ? "communication failure on the grid"
+                              : "failed on a rank of the grid";
+}
+
+static int summa_args(const cbg_tile* A, const cbg_tile* B, int sr, int algo, int exec) {
+  if (int rc = check_tile(A, true, "A")) return rc;
+  if (int rc = check_tile(B, true, "B")) return rc;
+  if ((sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) || (algo != CBG_DOUBLEBUFF && algo != CBG_SYNCH) ||
+      (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
+    return fail(CBG_ERR_INVALIDPARAMS, "bad summa parameters");
+  if (A->nnz >= INT32_MAX || B->nnz >= INT32_MAX) return fail(CBG_ERR_NOTSUPPORTED, "A/B tiles need nnz < 2^31");
+  return CBG_OK;
+}
+
 int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow, int sr,
                      int algo, int exec, cbg_tile* C) {
   if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
-  if (int rc = check_tile(A, true, "A")) return rc;
-  if (int rc = check_tile(B, true, "B")) return rc;
-  if (A == B) return fail(CBG_ERR_MATRIXALIAS, "inputs alias (make a temporary copy of one of them first)");
-  if (!C || (sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) || (algo != CBG_DOUBLEBUFF && algo != CBG_SYNCH) ||
-      (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
-    return fail(CBG_ERR_INVALIDPARAMS, "bad summa parameters");
+  int arg = summa_args(A, B, sr, algo, exec);
+  if (!arg && !C) arg = fail(CBG_ERR_INVALIDPARAMS, "C is NULL");
+  if (!arg && A == B) arg = fail(CBG_ERR_MATRIXALIAS, "inputs alias (make a temporary copy of one of them first)");
+  const std::string why = g_err;
   return guard([&]() -> int {
     cbg::thread_stats() = cbg::LocalStats{};
+    cbg::merge_stats() = cbg::MergeStats{};
+    if (arg) return fail(cbg::agree(g, arg), why);  // before any device call: peers must not block
     CBG_HIP(hipDeviceSynchronize());
+    cbg::step_error().clear();
     int rc = cbg::summa_spgemm(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, *C);
-    if (rc) return fail(rc, rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"
-                            : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
-                            : rc == CBG_ERR_NOTSQUARE   ? "staged SUMMA needs a square grid"
-                                                        : "summa failed");
+    if (rc) return fail(rc, cbg::step_error().empty() ? summa_msg(rc) : "this rank: " + cbg::step_error());
     return CBG_OK;
   });
 }
@@ -388,23 +415,36 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t 
 int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow,
                             int sr, int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
   if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
-  if (int rc = check_tile(A, true, "A")) return rc;
-  if (int rc = check_tile(B, true, "B")) return rc;  // A and B may alias: B is copied (ParFriends.h:547-549)
-  if ((!C && !fn) || (sr != CBG_PLUS_TIMES && sr != CBG_MIN_PLUS) || (algo != CBG_DOUBLEBUFF && algo != CBG_SYNCH) ||
-      (exec != CBG_EXEC_PANEL && exec != CBG_EXEC_STAGED))
-    return fail(CBG_ERR_INVALIDPARAMS, "bad phased summa parameters");
+  // A and B may alias: B is copied (ParFriends.h:547-549)
+  int arg = summa_args(A, B, sr, algo, exec);
+  if (!arg && !C && !fn) arg = fail(CBG_ERR_INVALIDPARAMS, "neither C nor a phase callback");
+  const std::string why = g_err;
   return guard([&]() -> int {
     cbg::thread_stats() = cbg::LocalStats{};
+    cbg::merge_stats() = cbg::MergeStats{};
+    if (arg) return fail(cbg::agree(g, arg), why);  // before any device call: peers must not block
     CBG_HIP(hipDeviceSynchronize());
+    cbg::step_error().clear();
     int rc = cbg::summa_spgemm_phased(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, phases, fn, user, C);
-    if (rc) return fail(rc, rc == CBG_ERR_DIMMISMATCH   ? "Can not multiply, dimensions does not match"
-                            : rc == CBG_ERR_MATRIXALIAS ? "Can not multiply, inputs alias"
-                            : rc == CBG_ERR_NOTSQUARE   ? "staged SUMMA needs a square grid"
-                            : rc == CBG_ERR_INVALIDPARAMS
-                                ? "phases: a B tile has fewer columns than phases, or a phase callback failed"
-                                : "phased summa failed");
+    if (rc) return fail(rc, cbg::step_error().empty() ? summa_msg(rc) : "this rank: " + cbg::step_error());
     return CBG_OK;
   });
+}
+
+int cbg_grid_agree(cbg_grid* g, int local_rc, int* agreed) {
+  if (!g || !agreed) return fail(CBG_ERR_INVALIDPARAMS, "grid or output is NULL");
+  return guard([&] {
+    *agreed = cbg::agree(g, local_rc);
+    return CBG_OK;
+  });
+}
+
+int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms) {
+  const cbg::MergeStats& m = cbg::merge_stats();
+  if (entries_in) *entries_in = m.entries_in;
+  if (entries_out) *entries_out = m.entries_out;
+  if (ms) *ms = m.ms;
+  return CBG_OK;
 }
 
 int cbg_grid_info(const cbg_grid* g, int* rank, int* nranks, int* rows, int* cols, int* prow, int* pcol);

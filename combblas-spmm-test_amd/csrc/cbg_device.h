@@ -243,6 +243,15 @@ __device__ __forceinline__ int lower_bound_g(const int32_t* __restrict__ a, int 
   return lo;
 }
 
+// the same over 64-bit positions (tiles with 2^31 or more entries)
+__device__ __forceinline__ int64_t lower_bound_g64(const int32_t* __restrict__ a, int64_t lo, int64_t hi, int key) {
+  while (lo < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
 // multiplicative hash into a power-of-two table
 template <int LOGT>
 __device__ __forceinline__ unsigned hash_slot(int key) {

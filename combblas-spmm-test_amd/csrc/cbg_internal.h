@@ -32,22 +32,62 @@ struct HipError : std::runtime_error {
 // Caching device allocator: blocks are rounded up (>= 2 MiB granules for big
 // requests) and recycled by size so that repeated multiplies never touch
 // hipMalloc/hipFree in steady state (cdna_hip_programming.md Guideline 9).
+//
+// Growable arrays (reserve_growable/grow) are a reserved virtual range whose
+// physical pages are mapped on demand (hipMemAddressReserve + hipMemCreate +
+// hipMemMap): a C tile assembled from several multiplies (pipeline pieces,
+// merge chunks) is written in place, with no concatenation copy, and holds
+// only the memory it uses.  A freed growable block stays mapped in the cache
+// (like the hipMalloc blocks) and is handed out again, so steady-state calls
+// map nothing; trim() (also run before an allocation is retried on OOM)
+// unmaps and releases them.
 class DevicePool {
  public:
   void* alloc(size_t bytes);
   void free(void* p);
   void trim();  // release every cached block
+  void* reserve_growable(size_t max_bytes);
+  void grow(void* base, size_t bytes);  // map [base, base + bytes)
   size_t bytes_in_use() const { return in_use_; }
   size_t bytes_cached() const { return cached_; }
   ~DevicePool() { trim(); }
 
  private:
+  struct Growable {
+    size_t reserved = 0, mapped = 0;
+    std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
+  };
+  void release_growable(void* base, Growable& g);
   std::mutex mu_;
   std::multimap<size_t, void*> free_;
   std::map<void*, size_t> live_;
+  std::map<void*, Growable> grow_;        // growable blocks in use
+  std::map<void*, Growable> grow_cache_;  // freed growable blocks, still mapped, reused first
   size_t in_use_ = 0, cached_ = 0;
 };
 DevicePool& pool();
+
+// cbg_tile.reserved bit: ir/val point into memory the tile does not own (an
+// EntryArena's ranges); tile_free_device then frees only cp and jc
+constexpr int32_t TILE_BORROWED_ENTRIES = 1;
+
+// where a local multiply puts C's row ids and values (default: fresh pool blocks)
+struct OutSink {
+  virtual void place(int64_t nnz, int32_t** ir, double** val) = 0;
+  virtual ~OutSink() = default;
+};
+// C entries of consecutive multiplies laid end to end in two growable arrays
+struct EntryArena : OutSink {
+  int32_t* ir = nullptr;
+  double* val = nullptr;
+  int64_t used = 0;
+  EntryArena();
+  ~EntryArena() override;
+  void place(int64_t nnz, int32_t** pir, double** pval) override;
+  void detach() { ir = nullptr; val = nullptr; used = 0; }
+  EntryArena(const EntryArena&) = delete;
+  EntryArena& operator=(const EntryArena&) = delete;
+};
 
 // RAII device buffer from the pool
 template <class T>
@@ -99,9 +139,17 @@ struct LocalStats {
 };
 // Every call accumulates into the calling thread's stats (reset by the C ABI
 // at the start of each public entry point); `st` optionally receives this call's.
+// sink: where C's entries go (C.reserved gets TILE_BORROWED_ENTRIES).
 void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s,
-                  LocalStats* st = nullptr);
+                  LocalStats* st = nullptr, OutSink* sink = nullptr);
 LocalStats& thread_stats();
+// merges run as products (cbg_merge.hip) but are not SpGEMM work: their
+// multiplies are kept out of thread_stats() and summed here instead
+struct MergeStats {
+  int64_t entries_in = 0, entries_out = 0;
+  double ms = 0;
+};
+MergeStats& merge_stats();
 // A-side preparation (column maps of A) kept across the local multiplies of
 // one MemEfficientSpGEMM call, whose phases all multiply the same A: between
 // aprep_begin() and aprep_end() on a thread, a local multiply whose A has the
@@ -118,13 +166,39 @@ void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t 
 void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s);
 
 // multiway merge of column-sorted partial tiles (cbg_merge.hip)
+// int64 entry counts: column chunks of < 2^30 stacked entries (CBG_MERGE_CHUNK
+// overrides) each run as one product into an EntryArena
 void merge_tiles(const std::vector<cbg_tile>& parts, int64_t m, int64_t n, int semiring, cbg_tile& C,
                  hipStream_t s);
 
 // tile helpers (cbg_tile.hip)
 void tile_free_device(cbg_tile& t);
 void tile_alloc_device(cbg_tile& t, int64_t m, int64_t n, int64_t nnz, int64_t nzc);
+// owner of a device tile inside host loops: freed on scope exit (exceptions included)
+struct TileGuard {
+  cbg_tile t{};
+  TileGuard() = default;
+  explicit TileGuard(const cbg_tile& x) : t(x) {}
+  ~TileGuard();
+  cbg_tile release() {
+    cbg_tile r = t;
+    t = cbg_tile{};
+    return r;
+  }
+  TileGuard(TileGuard&& o) noexcept : t(o.release()) {}
+  TileGuard& operator=(TileGuard&& o) noexcept;
+  TileGuard(const TileGuard&) = delete;
+  TileGuard& operator=(const TileGuard&) = delete;
+};
 void tile_split_cols(const cbg_tile& T, int64_t cut, cbg_tile& L, cbg_tile& R, hipStream_t s);
+// columns [a, b) / rows [a, b) of T as a new tile (re-based), one copy
+void tile_slice_cols(const cbg_tile& T, int64_t a, int64_t b, cbg_tile& out, hipStream_t s);
+void tile_slice_rows(const cbg_tile& T, int64_t a, int64_t b, cbg_tile& out, hipStream_t s);
+// column concatenation of tiles whose entries already lie end to end in
+// `arena` (parts[k].ir == arena.ir + sum of the earlier parts' nnz): only cp
+// and jc are built; `out` takes over the arena's arrays
+void tile_assemble_cols(const std::vector<cbg_tile>& parts, const std::vector<int64_t>& col_off, int64_t m,
+                        int64_t n, EntryArena& arena, cbg_tile& out, hipStream_t s);
 void tile_split_rows(const cbg_tile& T, int64_t cut, cbg_tile& Top, cbg_tile& Bot, hipStream_t s);
 void tile_concat_cols(const std::vector<cbg_tile>& parts, const std::vector<int64_t>& col_off, int64_t m,
                       int64_t n, cbg_tile& out, hipStream_t s);

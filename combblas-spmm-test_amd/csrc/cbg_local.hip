@@ -1465,7 +1465,8 @@ __global__ void k_col_scatter(int64_t n, const int32_t* __restrict__ cnt, const 
 // ----------------------------------------------------------------------------
 // host orchestration
 // ----------------------------------------------------------------------------
-void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st);
+void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st,
+                       OutSink* sink);
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 static int device_cus() {
@@ -1796,9 +1797,10 @@ LocalStats& thread_stats() {
   return t;
 }
 
-void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st) {
+void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st,
+                  OutSink* sink) {
   LocalStats mine;
-  local_spgemm_impl(A, B, semiring, C, s, &mine);
+  local_spgemm_impl(A, B, semiring, C, s, &mine, sink);
   LocalStats& t = thread_stats();
   t.flops += mine.flops;
   t.nnz += mine.nnz;
@@ -1809,7 +1811,8 @@ void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& 
   if (st) *st = mine;
 }
 
-void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st) {
+void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st,
+                       OutSink* sink) {
   C = cbg_tile{};
   C.m = A.m;
   C.n = B.n;
@@ -1819,6 +1822,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (st) *st = LocalStats{};
     return;
   }
+  TileGuard Cg;  // C's arrays until the multiply has completed (exceptions included)
   DeferredFree df;
   // side stream for the small-column bins (independent of the big columns)
   static thread_local hipStream_t side = nullptr;
@@ -1840,10 +1844,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipEventRecord(ev_join, side));
     CBG_HIP(hipStreamWaitEvent(main, ev_join, 0));
   };
-  hipEvent_t ev0, ev1, ev2;
-  CBG_HIP(hipEventCreate(&ev0));
-  CBG_HIP(hipEventCreate(&ev1));
-  CBG_HIP(hipEventCreate(&ev2));
+  // timing events, created once per thread and reused by every multiply
+  static thread_local hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  if (!ev0) {
+    CBG_HIP(hipEventCreate(&ev0));
+    CBG_HIP(hipEventCreate(&ev1));
+    CBG_HIP(hipEventCreate(&ev2));
+  }
   CBG_HIP(hipEventRecord(ev0, s));
   const int64_t nz = B.nzc;
   // A column map (reused across the phases of one MemEfficientSpGEMM)
@@ -2021,8 +2028,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   // output arrays
   C.nnz = nnzc;
-  C.ir = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nnzc, 1)));
-  C.val = static_cast<double*>(pool().alloc(sizeof(double) * std::max<int64_t>(nnzc, 1)));
+  if (sink) {
+    sink->place(nnzc, &C.ir, &C.val);
+    C.reserved |= TILE_BORROWED_ENTRIES;
+  } else {
+    C.ir = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nnzc, 1)));
+    C.val = static_cast<double*>(pool().alloc(sizeof(double) * std::max<int64_t>(nnzc, 1)));
+  }
+  Cg.t = C;
   // numeric
   Binned nbn;
   bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
@@ -2045,6 +2058,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   C.nzc = nzcC;
   C.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzcC + 1)));
   C.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzcC, 1)));
+  Cg.t = C;
   hipLaunchKernelGGL(k_col_scatter, dim3(nblk(nz + 1, 256)), dim3(256), 0, s, nz, cnt.p, pos.p, B.jc, colptr.p, C.jc,
                      C.cp);
   CBG_HIP(hipEventRecord(ev2, s));
@@ -2090,9 +2104,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemcpy(&tot, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost));
     st->flops = tot;
   }
-  (void)hipEventDestroy(ev0);
-  (void)hipEventDestroy(ev1);
-  (void)hipEventDestroy(ev2);
+  Cg.release();  // completed: the caller owns C
 }
 
 }  // namespace cbg

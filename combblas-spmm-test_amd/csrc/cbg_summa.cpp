@@ -15,15 +15,36 @@
 //            No partial products, no merge (the reference's dominant cost,
 //            69 % of DoubleBuff at 1x1).  Works on any pr x pc grid because
 //            the inner coordinates are global.
-//   STAGED : the reference's stage structure on square grids (sqrt(P) stages
-//            for Synch, 2 sqrt(P) half-tile stages for DoubleBuff); the
+//            The B block column arrives in column pieces: the broadcast of
+//            piece p+1 runs on the comm stream while piece p multiplies on
+//            the compute stream (double buffering), and the pieces' C entries
+//            are written end to end into one growable arena (no copy).
+//   STAGED : the reference's stage structure (sqrt(P) stages for Synch,
+//            2 sqrt(P) half-tile stages for DoubleBuff on square grids),
+//            generalized to pr x pc grids by cutting the inner dimension at
+//            the union of A's column-block and B's row-block boundaries; the
 //            broadcast of stage s+1 runs on the comm stream while stage s
 //            multiplies on the compute stream; partial products are merged
-//            on device (cbg_merge.hip).
+//            on device (cbg_merge.hip, 64-bit entry counts).
+//
+// Failure semantics.  The reference MPI_Aborts the whole job on a failed
+// check (ParFriends.h:160-183, SpDefs.h:69-76).  Here every collective entry
+// point agrees on a return code: after each local step the ranks take the
+// maximum of their codes over the world (agree()), so a rank-local failure
+// (an OOM inside the local multiply, a receive buffer that cannot be
+// allocated, a HIP error) makes every rank leave the call with that code,
+// after the collectives already posted have drained, instead of the others
+// blocking in the next broadcast.  Communicator failures (an RCCL async
+// error, or no progress for CBG_COMM_TIMEOUT_S seconds, default 600) abort
+// the grid's communicators (ncclCommAbort); the grid is then unusable and
+// every later call returns CBG_ERR_RCCL.
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <memory>
+#include <thread>
 
 #include "cbg_internal.h"
 
@@ -48,6 +69,9 @@ struct cbg_grid {
   ncclComm_t world = nullptr, row = nullptr, col = nullptr;
   hipStream_t compute = nullptr, comm = nullptr;
   hipEvent_t ev_comm = nullptr;
+  bool broken = false;  // communicators aborted: every later collective fails
+  int64_t calls = 0;    // SUMMA calls made on this grid (fault-injection index)
+  bool fault_armed = false;
 };
 
 namespace cbg {
@@ -104,7 +128,12 @@ cbg_grid* grid_create_host(int rank, int nranks, int rows, int cols, const cbg_h
   g->pcol = rank % cols;
   g->host_mode = true;
   g->hc = *hc;
-  grid_setup_streams(g.get());
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
+    grid_setup_streams(g.get());
+  } else {
+    (void)hipGetLastError();  // no device: only the host collectives (agree, barrier) are usable
+  }
   return g.release();
 }
 
@@ -122,33 +151,97 @@ void grid_destroy(cbg_grid* g) {
 // ---------------------------------------------------------------------------
 // collectives
 // ---------------------------------------------------------------------------
-static void host_check(int rc, const char* what) {
-  if (rc != 0) throw HipError(std::string("host transport ") + what + " failed", CBG_ERR_RCCL);
+static void host_check(cbg_grid* g, int rc, const char* what) {
+  if (rc != 0) {
+    g->broken = true;  // a peer is gone or the transport failed: no later call can agree
+    throw HipError(std::string("host transport ") + what + " failed", CBG_ERR_RCCL);
+  }
+}
+
+static double comm_timeout_s() {
+  static const char* e = getenv("CBG_COMM_TIMEOUT_S");
+  const double t = e ? atof(e) : 600.0;
+  return t > 0 ? t : 600.0;
+}
+
+// ncclCommAbort on every communicator of the grid (pending operations are
+// cancelled); the grid is unusable afterwards
+static void abort_comms(cbg_grid* g) {
+  for (ncclComm_t* c : {&g->row, &g->col, &g->world})
+    if (*c) {
+      (void)ncclCommAbort(*c);
+      *c = nullptr;
+    }
+  g->broken = true;
+}
+
+static void check_usable(cbg_grid* g) {
+  if (g->broken) throw HipError("grid communicators were aborted after an earlier failure", CBG_ERR_RCCL);
+}
+
+// Wait for the comm stream (the caller's collectives) with a watchdog:
+// an RCCL async error on any communicator, or no completion within
+// CBG_COMM_TIMEOUT_S, aborts the communicators instead of hanging.
+static void wait_comm(cbg_grid* g) {
+  if (g->host_mode) {
+    CBG_HIP(hipStreamSynchronize(g->comm));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const double limit = comm_timeout_s();
+  int spins = 0;
+  for (;;) {
+    hipError_t q = hipStreamQuery(g->comm);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) {
+      (void)hipGetLastError();
+      abort_comms(g);
+      throw HipError(std::string("comm stream: ") + hipGetErrorString(q), CBG_ERR_HIP);
+    }
+    for (ncclComm_t c : {g->world, g->row, g->col}) {
+      ncclResult_t ae = ncclSuccess;
+      if (c && ncclCommGetAsyncError(c, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+        abort_comms(g);
+        throw HipError(std::string("RCCL async error: ") + ncclGetErrorString(ae), CBG_ERR_RCCL);
+      }
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > limit) {
+      abort_comms(g);
+      throw HipError("collective made no progress for " + std::to_string((int)limit) +
+                         " s (CBG_COMM_TIMEOUT_S); communicators aborted",
+                     CBG_ERR_RCCL);
+    }
+    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 20));
+  }
 }
 
 // allgather of n int64 per rank (host buffers)
 void allgather_i64(cbg_grid* g, int which, const int64_t* in, int64_t* out, int n) {
+  check_usable(g);
   const int P = comm_size(g, which);
-  if (P == 1) {
-    std::memcpy(out, in, sizeof(int64_t) * n);
-    return;
-  }
   if (g->host_mode) {
-    host_check(g->hc.allgather(g->hc.user, which, in, out, sizeof(int64_t) * n), "allgather");
+    if (P == 1) {
+      std::memcpy(out, in, sizeof(int64_t) * n);
+      return;
+    }
+    host_check(g, g->hc.allgather(g->hc.user, which, in, out, sizeof(int64_t) * n), "allgather");
     return;
   }
+  // RCCL: executed for one-rank communicators too (a 1x1 RCCL grid runs the same calls)
   DBuf<int64_t> d(P * n + n);
   CBG_HIP(hipMemcpyAsync(d.p + P * n, in, sizeof(int64_t) * n, hipMemcpyHostToDevice, g->comm));
   CBG_NCCL(ncclAllGather(d.p + P * n, d.p, n, ncclInt64, pick(g, which), g->comm));
   CBG_HIP(hipMemcpyAsync(out, d.p, sizeof(int64_t) * P * n, hipMemcpyDeviceToHost, g->comm));
-  CBG_HIP(hipStreamSynchronize(g->comm));
+  wait_comm(g);
 }
 
 void allreduce_f64(cbg_grid* g, double* v, bool max) {
-  if (g->nranks == 1) return;
+  check_usable(g);
   if (g->host_mode) {
+    if (g->nranks == 1) return;
     std::vector<double> all(g->nranks);
-    host_check(g->hc.allgather(g->hc.user, COMM_WORLD, v, all.data(), sizeof(double)), "allgather");
+    host_check(g, g->hc.allgather(g->hc.user, COMM_WORLD, v, all.data(), sizeof(double)), "allgather");
     double r = all[0];
     for (double x : all) r = max ? std::max(r, x) : r + x;
     *v = r;
@@ -158,11 +251,10 @@ void allreduce_f64(cbg_grid* g, double* v, bool max) {
   CBG_HIP(hipMemcpyAsync(d.p, v, sizeof(double), hipMemcpyHostToDevice, g->comm));
   CBG_NCCL(ncclAllReduce(d.p, d.p, 1, ncclFloat64, max ? ncclMax : ncclSum, g->world, g->comm));
   CBG_HIP(hipMemcpyAsync(v, d.p, sizeof(double), hipMemcpyDeviceToHost, g->comm));
-  CBG_HIP(hipStreamSynchronize(g->comm));
+  wait_comm(g);
 }
 
 void allreduce_sum_i64(cbg_grid* g, int64_t* v) {
-  if (g->nranks == 1) return;
   std::vector<int64_t> all(g->nranks);
   allgather_i64(g, COMM_WORLD, v, all.data(), 1);
   int64_t s = 0;
@@ -175,21 +267,78 @@ void barrier(cbg_grid* g) {
   allreduce_f64(g, &z, true);
 }
 
+// The agreed code of a collective step: max over the world of the ranks'
+// local codes (0 = success).  Every rank calls it at the same points, so a
+// failed rank never leaves its peers blocked in a broadcast it skipped.
+int agree(cbg_grid* g, int rc) {
+  int64_t v = rc, w = 0;
+  std::vector<int64_t> all(g->nranks);
+  allgather_i64(g, COMM_WORLD, &v, all.data(), 1);
+  for (auto x : all) w = std::max(w, x);
+  return (int)w;
+}
+
+// Test hook (CBG_FAULT_INJECT="rank:k1,k2,..."): in the listed SUMMA calls
+// that rank `rank` makes on a grid (counted from 0 over the grid's life), the
+// first local multiply fails as an out-of-memory would.
+static void arm_fault(cbg_grid* g) {
+  static const char* e = getenv("CBG_FAULT_INJECT");
+  const int64_t k = g->calls++;
+  g->fault_armed = false;
+  if (!e) return;
+  const char* c = strchr(e, ':');
+  if (!c || atoi(e) != g->rank) return;
+  for (const char* q = c + 1; *q;) {
+    char* end = nullptr;
+    const long long at = strtoll(q, &end, 10);
+    if (end == q) break;
+    if (at == k) g->fault_armed = true;
+    q = *end == ',' ? end + 1 : end;
+  }
+}
+static void maybe_inject_fault(cbg_grid* g) {
+  if (!g->fault_armed) return;
+  g->fault_armed = false;
+  throw HipError("injected fault (CBG_FAULT_INJECT) in SUMMA call " + std::to_string(g->calls - 1), CBG_ERR_OOM);
+}
+
+// code of a failure inside a collective step (the step's exception is not
+// rethrown: the caller must still reach the next agree()); the first message
+// of the calling thread is kept for cbg_last_error()
+std::string& step_error() {
+  static thread_local std::string m;
+  return m;
+}
+template <class F>
+static int step(F&& f) {
+  try {
+    f();
+    return CBG_OK;
+  } catch (const HipError& e) {
+    if (std::getenv("CBG_DEBUG_ERRORS")) std::fprintf(stderr, "[cbg] %s\n", e.what());
+    if (step_error().empty()) step_error() = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    if (step_error().empty()) step_error() = "host allocation failed";
+    return CBG_ERR_OOM;
+  }
+}
+
 // Broadcast a tile within a row/col communicator (BCastMatrix: the essentials
 // {m,n,nnz,nzc} are known from the allgather; Create(ess) then 4 broadcasts).
-// `t` holds the root's tile on the root; on the others it is allocated here.
-// Enqueued on g->comm; the caller orders the consumer with g->ev_comm.
+// `t` is the root's tile on the root and an allocated receive tile elsewhere.
+// RCCL: enqueued on g->comm (callers group the broadcasts of one step and
+// order the consumer with g->ev_comm); host transport: synchronous.
 static void bcast_tile(cbg_grid* g, int which, int root, const int64_t ess[4], cbg_tile& t, bool mine) {
-  if (!mine) tile_alloc_device(t, ess[0], ess[1], ess[2], ess[3]);
   const int64_t nnz = ess[2], nzc = ess[3];
-  if (comm_size(g, which) == 1) return;
   if (g->host_mode) {
+    if (comm_size(g, which) == 1) return;
     CBG_HIP(hipStreamSynchronize(g->comm));
     auto hb = [&](void* dptr, size_t bytes) {
       if (bytes == 0) return;
       std::vector<char> h(bytes);
       if (mine) CBG_HIP(hipMemcpy(h.data(), dptr, bytes, hipMemcpyDeviceToHost));
-      host_check(g->hc.bcast(g->hc.user, which, h.data(), bytes, root), "bcast");
+      host_check(g, g->hc.bcast(g->hc.user, which, h.data(), bytes, root), "bcast");
       if (!mine) CBG_HIP(hipMemcpy(dptr, h.data(), bytes, hipMemcpyHostToDevice));
     };
     hb(t.cp, sizeof(int64_t) * (nzc + 1));
@@ -198,15 +347,27 @@ static void bcast_tile(cbg_grid* g, int which, int root, const int64_t ess[4], c
     hb(t.val, sizeof(double) * nnz);
     return;
   }
+  // RCCL, one-rank communicators included
   ncclComm_t c = pick(g, which);
-  CBG_NCCL(ncclGroupStart());
   CBG_NCCL(ncclBroadcast(t.cp, t.cp, nzc + 1, ncclInt64, root, c, g->comm));
   if (nzc) CBG_NCCL(ncclBroadcast(t.jc, t.jc, nzc, ncclInt32, root, c, g->comm));
   if (nnz) {
     CBG_NCCL(ncclBroadcast(t.ir, t.ir, nnz, ncclInt32, root, c, g->comm));
     CBG_NCCL(ncclBroadcast(t.val, t.val, nnz, ncclFloat64, root, c, g->comm));
   }
-  CBG_NCCL(ncclGroupEnd());
+}
+
+// one step's broadcasts as one RCCL group
+template <class F>
+static void bcast_group(cbg_grid* g, F&& f) {
+  if (!g->host_mode) CBG_NCCL(ncclGroupStart());
+  try {
+    f();
+  } catch (...) {
+    if (!g->host_mode) (void)ncclGroupEnd();
+    throw;
+  }
+  if (!g->host_mode) CBG_NCCL(ncclGroupEnd());
 }
 
 static void tile_ess(const cbg_tile& t, int64_t e[4]) {
@@ -216,201 +377,386 @@ static void tile_ess(const cbg_tile& t, int64_t e[4]) {
   e[3] = t.nzc;
 }
 
+static void alloc_like(cbg_tile& t, const int64_t e[4]) { tile_alloc_device(t, e[0], e[1], e[2], e[3]); }
+
+// ---------------------------------------------------------------------------
+// PANEL (pipelined): Mult_AnXBn_DoubleBuff / _Synch as ONE local multiply of
+// the A block row by the B block column (ParFriends.h:845-964 computes the
+// same sum of stage products), the B block column arriving in column pieces
+// cuts[0] = 0 < cuts[1] < ... < cuts[np] = B.n.  Comm stream, every rank in
+// the same order: [A row broadcasts][piece 0][agree][piece 1][agree]...;
+// the compute stream multiplies piece p while piece p+1 is broadcast.
+// fn != NULL: each piece's C goes to fn and is freed (MemEfficientSpGEMM
+// phases); else the pieces' entries go end to end into one EntryArena and C
+// is their column concatenation (ColConcatenate without a copy).
+// ---------------------------------------------------------------------------
+static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
+                       const std::vector<int64_t>& cuts, cbg_phase_fn fn, void* user, cbg_tile* C) {
+  const int np = (int)cuts.size() - 1;
+  const int pr = g->pr, pc = g->pc;
+  hipStream_t cs = g->compute;
+  // my B pieces (column slices; the whole tile when np == 1)
+  std::vector<TileGuard> own(np);
+  std::vector<cbg_tile> piece(np);
+  int rc = step([&] {
+    for (int p = 0; p < np; ++p) {
+      if (np == 1) {
+        piece[p] = B;
+      } else {
+        tile_slice_cols(B, cuts[p], cuts[p + 1], own[p].t, cs);
+        piece[p] = own[p].t;
+      }
+    }
+  });
+  if ((rc = agree(g, rc))) return rc;
+  // GetSetSizes: A tiles along my grid row, every piece of the B tiles along my grid column
+  int64_t ea[4];
+  tile_ess(A, ea);
+  std::vector<int64_t> eb((size_t)4 * np);
+  for (int p = 0; p < np; ++p) tile_ess(piece[p], &eb[4 * p]);
+  std::vector<int64_t> EA((size_t)4 * pc), EB((size_t)4 * np * pr);
+  allgather_i64(g, COMM_ROW, ea, EA.data(), 4);
+  allgather_i64(g, COMM_COL, eb.data(), EB.data(), 4 * np);
+  auto eB = [&](int s, int p) { return &EB[(size_t)4 * (s * np + p)]; };
+  int64_t kA = 0, kB = 0;
+  for (int s = 0; s < pc; ++s) kA += EA[4 * s + 1];
+  for (int s = 0; s < pr; ++s) kB += eB(s, 0)[0];
+  if ((rc = agree(g, (kA != A_gncol || kB != B_gnrow) ? CBG_ERR_DIMMISMATCH : CBG_OK))) return rc;
+  std::vector<int64_t> aoff(pc + 1, 0), boff(pr + 1, 0);
+  for (int s = 0; s < pc; ++s) aoff[s + 1] = aoff[s] + EA[4 * s + 1];
+  for (int s = 0; s < pr; ++s) boff[s + 1] = boff[s] + eB(s, 0)[0];
+
+  std::vector<TileGuard> Ar(pc);
+  std::vector<std::vector<TileGuard>> Bc(np);
+  for (auto& v : Bc) v.resize(pr);
+  auto alloc_piece = [&](int p) {
+    for (int s = 0; s < pr; ++s)
+      if (s != g->prow) alloc_like(Bc[p][s].t, eB(s, p));
+  };
+  auto post_piece = [&](int p) {
+    bcast_group(g, [&] {
+      for (int s = 0; s < pr; ++s)
+        bcast_tile(g, COMM_COL, s, eB(s, p), s == g->prow ? piece[p] : Bc[p][s].t, s == g->prow);
+    });
+    CBG_HIP(hipEventRecord(g->ev_comm, g->comm));
+  };
+  rc = step([&] {
+    for (int s = 0; s < pc; ++s)
+      if (s != g->pcol) alloc_like(Ar[s].t, &EA[4 * s]);
+    alloc_piece(0);
+  });
+  if ((rc = agree(g, rc))) return rc;
+  // from here on every rank has posted the same broadcasts: errors are
+  // recorded, agreed on at the next step, and the comm stream is drained
+  int local = step([&] {
+    bcast_group(g, [&] {
+      for (int s = 0; s < pc; ++s) {
+        cbg_tile& t = s == g->pcol ? const_cast<cbg_tile&>(A) : Ar[s].t;
+        bcast_tile(g, COMM_ROW, s, &EA[4 * s], t, s == g->pcol);
+      }
+    });
+    post_piece(0);
+  });
+  APrepScope aprep_scope;  // every piece multiplies the same A panel: keep its column maps
+  std::unique_ptr<EntryArena> arena;
+  if (!fn && np > 1) arena.reset(new EntryArena());
+  std::vector<TileGuard> outs;
+  std::vector<cbg_tile> outv;
+  TileGuard Apanel;
+  const cbg_tile* Ause = &A;
+  int cb_rc = 0;
+  for (int p = 0; p < np && !rc; ++p) {
+    local = std::max(local, step([&] { CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0)); }));
+    if (p + 1 < np) {
+      // every rank holds piece p+1's receive buffers before anyone posts it
+      local = std::max(local, step([&] { alloc_piece(p + 1); }));
+      if ((rc = agree(g, local))) break;
+      local = std::max(local, step([&] { post_piece(p + 1); }));
+    }
+    if (local) continue;  // agreed at the next step
+    local = step([&] {
+      maybe_inject_fault(g);
+      if (p == 0 && pc > 1) {
+        std::vector<cbg_tile> parts(pc);
+        for (int s = 0; s < pc; ++s) parts[s] = s == g->pcol ? A : Ar[s].t;
+        tile_concat_cols(parts, std::vector<int64_t>(aoff.begin(), aoff.end() - 1), A.m, A_gncol, Apanel.t, cs);
+        for (auto& t : Ar) tile_free_device(t.t);
+        Ause = &Apanel.t;
+      }
+      TileGuard Bp;
+      const cbg_tile* Buse = &piece[p];
+      if (pr > 1) {
+        std::vector<cbg_tile> parts(pr);
+        for (int s = 0; s < pr; ++s) parts[s] = s == g->prow ? piece[p] : Bc[p][s].t;
+        tile_concat_rows(parts, std::vector<int64_t>(boff.begin(), boff.end() - 1), B_gnrow, cuts[p + 1] - cuts[p],
+                         Bp.t, cs);
+        Buse = &Bp.t;
+      }
+      TileGuard Cp;
+      local_spgemm(*Ause, *Buse, sr, Cp.t, cs, nullptr, arena.get());
+      for (auto& t : Bc[p]) tile_free_device(t.t);
+      tile_free_device(own[p].t);
+      if (fn) {
+        CBG_HIP(hipStreamSynchronize(cs));
+        const int r = fn(user, p, cuts[p], &Cp.t);
+        if (r && !cb_rc) cb_rc = r;
+      } else {
+        outv.push_back(Cp.t);
+        outs.push_back(std::move(Cp));
+      }
+    });
+  }
+  if (!rc) rc = agree(g, local);
+  if (rc) {
+    if (!g->broken) wait_comm(g);  // posted broadcasts complete before their buffers are released
+    return rc;
+  }
+  if (fn) return cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK;
+  rc = step([&] {
+    if (np == 1) {
+      *C = outs[0].release();
+    } else {
+      std::vector<int64_t> off(cuts.begin(), cuts.end() - 1);
+      tile_assemble_cols(outv, off, A.m, B.n, *arena, *C, cs);
+    }
+  });
+  return agree(g, rc);
+}
+
+// ---------------------------------------------------------------------------
+// STAGED: the reference's stages (ParFriends.h:845-964 DoubleBuff: A split by
+// columns at n/2 and B by rows at m/2, 2 sqrt(P) stages; :1004-1108 Synch:
+// sqrt(P) stages), generalized to pr x pc grids: the inner dimension is cut
+// at the union of A's column-block and B's row-block boundaries (lcm(pr, pc)
+// ranges for power-of-two grids), DoubleBuff halves every range and runs all
+// first halves before all second halves.  Stage s+1's broadcasts are posted
+// before stage s multiplies; the partials are merged on device (MergeAll /
+// MultiwayMerge, 64-bit entry counts).  On square grids the stages, their
+// roots and their pieces are exactly the reference's.
+// ---------------------------------------------------------------------------
+static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
+                        int algo, cbg_tile& C) {
+  const int pr = g->pr, pc = g->pc;
+  hipStream_t cs = g->compute;
+  const int64_t K = A_gncol;
+  auto blk = [](int64_t ext, int np_, int i) {  // SpParMat::Owner block start
+    return i >= np_ ? ext : (int64_t)i * (ext / np_);
+  };
+  std::vector<int64_t> bnd;
+  for (int s = 0; s <= pc; ++s) bnd.push_back(blk(K, pc, s));
+  for (int s = 0; s <= pr; ++s) bnd.push_back(blk(K, pr, s));
+  std::sort(bnd.begin(), bnd.end());
+  bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+  struct Stage {
+    int64_t lo, hi;
+    int sa, sb;
+  };
+  auto owner = [&](int64_t k, int np_) {  // block of inner index k
+    int s = (int)std::min<int64_t>(np_ - 1, K / np_ ? k / (K / np_) : np_ - 1);
+    while (s > 0 && blk(K, np_, s) > k) --s;
+    while (s + 1 < np_ && blk(K, np_, s + 1) <= k) ++s;
+    return s;
+  };
+  std::vector<Stage> st;
+  for (int half = 0; half < (algo == CBG_DOUBLEBUFF ? 2 : 1); ++half)
+    for (size_t j = 0; j + 1 < bnd.size(); ++j) {
+      int64_t lo = bnd[j], hi = bnd[j + 1];
+      if (hi <= lo) continue;
+      const int sa = owner(lo, pc), sb = owner(lo, pr);
+      if (algo == CBG_DOUBLEBUFF) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (half == 0) hi = mid; else lo = mid;
+      }
+      st.push_back({lo, hi, sa, sb});
+    }
+  const int S = (int)st.size();
+  // my pieces: A columns of the stages rooted at my grid column, B rows of those rooted at my grid row
+  std::vector<TileGuard> myA(S), myB(S);
+  int rc = step([&] {
+    for (int s = 0; s < S; ++s) {
+      if (st[s].sa == g->pcol) {
+        const int64_t o = blk(K, pc, st[s].sa);
+        tile_slice_cols(A, st[s].lo - o, st[s].hi - o, myA[s].t, cs);
+      }
+      if (st[s].sb == g->prow) {
+        const int64_t o = blk(K, pr, st[s].sb);
+        tile_slice_rows(B, st[s].lo - o, st[s].hi - o, myB[s].t, cs);
+      }
+    }
+  });
+  if ((rc = agree(g, rc))) return rc;
+  std::vector<int64_t> ea((size_t)4 * S, 0), eb((size_t)4 * S, 0);
+  for (int s = 0; s < S; ++s) {
+    tile_ess(myA[s].t, &ea[4 * s]);
+    tile_ess(myB[s].t, &eb[4 * s]);
+  }
+  std::vector<int64_t> EA((size_t)4 * S * pc), EB((size_t)4 * S * pr);
+  allgather_i64(g, COMM_ROW, ea.data(), EA.data(), 4 * S);  // GetSetSizes (ParFriends.h:834-835 / :1025-1026)
+  allgather_i64(g, COMM_COL, eb.data(), EB.data(), 4 * S);
+  auto eA = [&](int s) { return &EA[(size_t)4 * (st[s].sa * S + s)]; };
+  auto eB = [&](int s) { return &EB[(size_t)4 * (st[s].sb * S + s)]; };
+  int64_t kA = 0, kB = 0;
+  for (int s = 0; s < S; ++s) {
+    kA += eA(s)[1];
+    kB += eB(s)[0];
+  }
+  if ((rc = agree(g, (kA != A_gncol || kB != B_gnrow) ? CBG_ERR_DIMMISMATCH : CBG_OK))) return rc;
+  std::vector<TileGuard> Ar(S), Bc(S);
+  auto alloc_stage = [&](int s) {
+    if (st[s].sa != g->pcol) alloc_like(Ar[s].t, eA(s));
+    if (st[s].sb != g->prow) alloc_like(Bc[s].t, eB(s));
+  };
+  auto post = [&](int s) {
+    bcast_group(g, [&] {
+      bcast_tile(g, COMM_ROW, st[s].sa, eA(s), st[s].sa == g->pcol ? myA[s].t : Ar[s].t, st[s].sa == g->pcol);
+      bcast_tile(g, COMM_COL, st[s].sb, eB(s), st[s].sb == g->prow ? myB[s].t : Bc[s].t, st[s].sb == g->prow);
+    });
+    CBG_HIP(hipEventRecord(g->ev_comm, g->comm));
+  };
+  rc = step([&] { alloc_stage(0); });
+  if ((rc = agree(g, rc))) return rc;
+  int local = step([&] { post(0); });
+  std::vector<TileGuard> partials;
+  std::vector<cbg_tile> pv;
+  for (int s = 0; s < S && !rc; ++s) {
+    local = std::max(local, step([&] { CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0)); }));
+    if (s + 1 < S) {
+      local = std::max(local, step([&] { alloc_stage(s + 1); }));
+      if ((rc = agree(g, local))) break;
+      local = std::max(local, step([&] { post(s + 1); }));
+    }
+    if (local) continue;
+    local = step([&] {
+      maybe_inject_fault(g);
+      const cbg_tile& a = st[s].sa == g->pcol ? myA[s].t : Ar[s].t;
+      const cbg_tile& b = st[s].sb == g->prow ? myB[s].t : Bc[s].t;
+      TileGuard P;
+      local_spgemm(a, b, sr, P.t, cs, nullptr);  // LocalHybridSpGEMM (ParFriends.h:888-891)
+      tile_free_device(Ar[s].t);
+      tile_free_device(Bc[s].t);
+      tile_free_device(myA[s].t);
+      tile_free_device(myB[s].t);
+      if (P.t.nnz > 0) {
+        pv.push_back(P.t);
+        partials.push_back(std::move(P));
+      }
+    });
+  }
+  if (!rc) rc = agree(g, local);
+  if (rc) {
+    if (!g->broken) wait_comm(g);
+    return rc;
+  }
+  // MergeAll (DoubleBuff, Friends.h:657-741) / MultiwayMerge (Synch, MultiwayMerge.h:409-526)
+  rc = step([&] {
+    if (pv.size() == 1) {
+      C = partials[0].release();
+    } else {
+      merge_tiles(pv, A.m, B.n, sr, C, cs);
+    }
+  });
+  return agree(g, rc);
+}
+
+// pieces of the pipelined PANEL multiply when C stays resident: the first
+// piece small (its broadcast is exposed), the rest behind its multiply.
+// CBG_PIPELINE=k: k equal pieces (1 = no pipelining); default: 1 without
+// communication (one grid cell), else 2 with a first piece of 1/8 of B's columns
+static std::vector<int64_t> pipeline_cuts(cbg_grid* g, int64_t n) {
+  static const char* e = getenv("CBG_PIPELINE");
+  int k = e ? atoi(e) : (g->pr * g->pc > 1 ? -2 : 1);
+  if (k == 0 || k == 1 || n < 16) return {0, n};
+  if (k == -2) return {0, n / 8, n};
+  k = (int)std::min<int64_t>(k, n);
+  std::vector<int64_t> c;
+  for (int i = 0; i <= k; ++i) c.push_back((int64_t)i * n / k);
+  return c;
+}
+
 // ---------------------------------------------------------------------------
 // Mult_AnXBn_{DoubleBuff,Synch}
 // ---------------------------------------------------------------------------
 int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr, int algo,
                  int exec, cbg_tile& C) {
-  // CheckSpGEMMCompliance (ParFriends.h:160-183)
-  if (A_gncol != B_gnrow) return CBG_ERR_DIMMISMATCH;
-  if (&A == &B || (A.ir == B.ir && A.nnz > 0)) return CBG_ERR_MATRIXALIAS;
-  // GetSetSizes: essentials of every A tile in my grid row, every B tile in my grid column
-  int64_t ea[4], eb[4];
-  tile_ess(A, ea);
-  tile_ess(B, eb);
-  std::vector<int64_t> EA((size_t)4 * g->pc), EB((size_t)4 * g->pr);
-  allgather_i64(g, COMM_ROW, ea, EA.data(), 4);
-  allgather_i64(g, COMM_COL, eb, EB.data(), 4);
-  int64_t kA = 0, kB = 0;
-  for (int s = 0; s < g->pc; ++s) kA += EA[4 * s + 1];
-  for (int s = 0; s < g->pr; ++s) kB += EB[4 * s + 0];
-  if (kA != A_gncol || kB != B_gnrow) return CBG_ERR_DIMMISMATCH;
-  const int64_t Cm = A.m, Cn = B.n;
-  hipStream_t cs = g->compute;
-
+  check_usable(g);
+  arm_fault(g);
+  // CheckSpGEMMCompliance (ParFriends.h:160-183), agreed over the grid
+  int rc = A_gncol != B_gnrow ? CBG_ERR_DIMMISMATCH
+           : (&A == &B || (A.ir == B.ir && A.nnz > 0)) ? CBG_ERR_MATRIXALIAS
+           : CBG_OK;
+  if ((rc = agree(g, rc))) return rc;
   if (exec == CBG_EXEC_PANEL) {
-    // gather the A block row and the B block column
-    std::vector<cbg_tile> Ar(g->pc), Bc(g->pr);
-    std::vector<int64_t> aoff(g->pc), boff(g->pr);
-    int64_t o = 0;
-    for (int s = 0; s < g->pc; ++s) {
-      aoff[s] = o;
-      o += EA[4 * s + 1];
-      if (s == g->pcol) Ar[s] = A; else Ar[s] = cbg_tile{};
-      bcast_tile(g, COMM_ROW, s, &EA[4 * s], Ar[s], s == g->pcol);
-    }
-    o = 0;
-    for (int s = 0; s < g->pr; ++s) {
-      boff[s] = o;
-      o += EB[4 * s + 0];
-      if (s == g->prow) Bc[s] = B; else Bc[s] = cbg_tile{};
-      bcast_tile(g, COMM_COL, s, &EB[4 * s], Bc[s], s == g->prow);
-    }
-    CBG_HIP(hipStreamSynchronize(g->comm));
-    cbg_tile Ap{}, Bp{};
-    const cbg_tile* Ause = &A;
-    const cbg_tile* Buse = &B;
-    if (g->pc > 1) {
-      tile_concat_cols(Ar, aoff, Cm, A_gncol, Ap, cs);
-      Ause = &Ap;
-    }
-    if (g->pr > 1) {
-      tile_concat_rows(Bc, boff, B_gnrow, Cn, Bp, cs);
-      Buse = &Bp;
-    }
-    for (int s = 0; s < g->pc; ++s)
-      if (s != g->pcol) tile_free_device(Ar[s]);
-    for (int s = 0; s < g->pr; ++s)
-      if (s != g->prow) tile_free_device(Bc[s]);
-    local_spgemm(*Ause, *Buse, sr, C, cs, nullptr);
-    if (g->pc > 1) tile_free_device(Ap);
-    if (g->pr > 1) tile_free_device(Bp);
-    return CBG_OK;
+    // every rank cuts its B tile at the same relative places (tiles of one grid column share n)
+    return summa_panel(g, A, B, A_gncol, B_gnrow, sr, pipeline_cuts(g, B.n), nullptr, nullptr, &C);
   }
-
-  // ---------------- STAGED (reference stage structure, square grids) ----------------
-  if (g->pr != g->pc) return CBG_ERR_NOTSQUARE;
-  const int stages = g->pc;  // ProductGrid: innerdim = grcols
-  std::vector<cbg_tile> partials;
-  auto run_half = [&](const cbg_tile& Aseq, const cbg_tile& Bseq) {
-    int64_t a4[4], b4[4];
-    tile_ess(Aseq, a4);
-    tile_ess(Bseq, b4);
-    std::vector<int64_t> SA((size_t)4 * stages), SB((size_t)4 * stages);
-    allgather_i64(g, COMM_ROW, a4, SA.data(), 4);  // GetSetSizes (ParFriends.h:834-835 / :1025-1026)
-    allgather_i64(g, COMM_COL, b4, SB.data(), 4);
-    // double buffer: stage s+1's broadcast is enqueued on the comm stream
-    // before stage s's multiply runs on the compute stream
-    std::vector<cbg_tile> Ar(stages), Bc(stages);
-    auto post = [&](int s) {
-      Ar[s] = (s == g->pcol) ? Aseq : cbg_tile{};
-      Bc[s] = (s == g->prow) ? Bseq : cbg_tile{};
-      bcast_tile(g, COMM_ROW, s, &SA[4 * s], Ar[s], s == g->pcol);
-      bcast_tile(g, COMM_COL, s, &SB[4 * s], Bc[s], s == g->prow);
-    };
-    post(0);
-    for (int s = 0; s < stages; ++s) {
-      CBG_HIP(hipEventRecord(g->ev_comm, g->comm));
-      CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0));
-      if (s + 1 < stages) post(s + 1);
-      cbg_tile P{};
-      local_spgemm(Ar[s], Bc[s], sr, P, cs, nullptr);  // LocalHybridSpGEMM (ParFriends.h:888-891)
-      if (s != g->pcol) tile_free_device(Ar[s]);
-      if (s != g->prow) tile_free_device(Bc[s]);
-      if (P.nnz > 0) partials.push_back(P); else tile_free_device(P);
-    }
-  };
-  cbg_tile A1{}, A2{}, B1{}, B2{};
-  if (algo == CBG_DOUBLEBUFF) {
-    // A split by columns at n/2, B by rows at m/2 (ParFriends.h:823-829)
-    tile_split_cols(A, A.n / 2, A1, A2, cs);
-    tile_split_rows(B, B.m / 2, B1, B2, cs);
-    run_half(A1, B1);
-    run_half(A2, B2);
-    tile_free_device(A1);
-    tile_free_device(A2);
-    tile_free_device(B1);
-    tile_free_device(B2);
-  } else {
-    run_half(A, B);
-  }
-  // MergeAll (DoubleBuff, Friends.h:657-741) / MultiwayMerge (Synch, MultiwayMerge.h:409-526)
-  if (partials.size() == 1) {
-    C = partials[0];
-  } else {
-    merge_tiles(partials, Cm, Cn, sr, C, cs);
-    for (auto& p : partials) tile_free_device(p);
-  }
-  return CBG_OK;
+  return summa_staged(g, A, B, A_gncol, B_gnrow, sr, algo, C);
 }
-
 
 // ---------------------------------------------------------------------------
 // MemEfficientSpGEMM (ParFriends.h:449-730) minus its Markov-clustering pruning:
 // B's local tile is cut into `phases` column pieces like SpDCCols::ColSplit
-// (SpDCCols.cpp:936-970), each piece goes through summa_spgemm, and the phase
+// (SpDCCols.cpp:936-970), each piece goes through the SUMMA, and the phase
 // results are streamed to `fn` or column-concatenated (ColConcatenate,
 // ParFriends.h:724-725).  Column pieces keep every C column's products inside
-// one phase, so the result is identical to the unphased product.
+// one phase, so the result is identical to the unphased product.  PANEL: the
+// phases are the pipeline's pieces (A's row panel is gathered once, phase
+// p+1's B pieces are broadcast while phase p multiplies); STAGED: one staged
+// SUMMA per phase.
 // ---------------------------------------------------------------------------
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                         int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+  check_usable(g);
+  arm_fault(g);
   if (phases < 1 || phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
-  int64_t small = B.n < phases ? 1 : 0;              // ColSplit: "Matrix is too small to be splitted"
-  allreduce_sum_i64(g, &small);
-  if (small) return CBG_ERR_INVALIDPARAMS;
+  int rc = B.n < phases ? CBG_ERR_INVALIDPARAMS : CBG_OK;  // ColSplit: "Matrix is too small to be splitted"
+  if (A_gncol != B_gnrow) rc = CBG_ERR_DIMMISMATCH;
+  if ((rc = agree(g, rc))) return rc;
   hipStream_t cs = g->compute;
-  // column pieces of B: [p * (n / phases), (p + 1) * (n / phases)), the last takes the rest
-  std::vector<cbg_tile> pieces(phases);
-  std::vector<int64_t> off(phases);
-  const int64_t w = B.n / phases;
   // the reference copies B first, so A and B may alias here (ParFriends.h:547-549)
   const bool alias = (&A == &B) || (A.ir == B.ir && A.nnz > 0);
-  const bool copied = phases > 1 || alias;
-  if (!copied) {
-    pieces[0] = B;
-  } else if (phases == 1) {
-    cbg_tile right{};
-    tile_split_cols(B, B.n, pieces[0], right, cs);
-    tile_free_device(right);
-  } else {
-    cbg_tile rest = B;
-    for (int p = 0; p < phases - 1; ++p) {
-      cbg_tile left{}, right{};
-      tile_split_cols(rest, w, left, right, cs);
-      if (p > 0) tile_free_device(rest);
-      pieces[p] = left;
-      rest = right;
+  const int64_t w = B.n / phases;
+  std::vector<int64_t> cuts;
+  for (int p = 0; p < phases; ++p) cuts.push_back((int64_t)p * w);
+  cuts.push_back(B.n);
+  if (exec == CBG_EXEC_PANEL) {
+    TileGuard Bcopy;
+    const cbg_tile* Bu = &B;
+    if (alias) {
+      rc = step([&] { tile_slice_cols(B, 0, B.n, Bcopy.t, cs); });
+      if ((rc = agree(g, rc))) return rc;
+      Bu = &Bcopy.t;
     }
-    pieces[phases - 1] = rest;
+    return summa_panel(g, A, *Bu, A_gncol, B_gnrow, sr, cuts, fn, user, C);
   }
-  for (int p = 0; p < phases; ++p) off[p] = (int64_t)p * w;
-  std::vector<cbg_tile> parts;
+  std::vector<TileGuard> parts;
+  std::vector<cbg_tile> pv;
   int cb_rc = 0;
-  // every phase multiplies the caller's A itself when the PANEL execution needs
-  // no A row concatenation (one grid column): keep its column maps across the
-  // phases (other executions multiply per-stage / per-phase copies of A)
-  std::unique_ptr<APrepScope> aprep_scope;
-  if (exec == CBG_EXEC_PANEL && g->pc == 1) aprep_scope.reset(new APrepScope());
   for (int p = 0; p < phases; ++p) {
-    cbg_tile Cp{};
-    const int rc = summa_spgemm(g, A, pieces[p], A_gncol, B_gnrow, sr, algo, exec, Cp);
-    if (copied) tile_free_device(pieces[p]);
-    if (rc) {
-      for (int q = p + 1; q < phases; ++q)
-        if (copied) tile_free_device(pieces[q]);
-      for (auto& t : parts) tile_free_device(t);
-      return rc;
-    }
+    TileGuard piece, Cp;
+    rc = step([&] { tile_slice_cols(B, cuts[p], cuts[p + 1], piece.t, cs); });
+    if ((rc = agree(g, rc))) return rc;
+    rc = summa_staged(g, A, piece.t, A_gncol, B_gnrow, sr, algo, Cp.t);
+    if (rc) return rc;
     if (fn) {
       CBG_HIP(hipStreamSynchronize(cs));
-      const int r = fn(user, p, off[p], &Cp);
+      const int r = fn(user, p, cuts[p], &Cp.t);
       if (r && !cb_rc) cb_rc = r;
-      tile_free_device(Cp);
     } else {
-      parts.push_back(Cp);
+      pv.push_back(Cp.t);
+      parts.push_back(std::move(Cp));
     }
   }
   if (fn) return cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK;
-  if (parts.size() == 1) {
-    *C = parts[0];
-  } else {
-    tile_concat_cols(parts, off, A.m, B.n, *C, cs);
-    for (auto& t : parts) tile_free_device(t);
-  }
-  return CBG_OK;
+  rc = step([&] {
+    if (pv.size() == 1) {
+      *C = parts[0].release();
+    } else {
+      std::vector<int64_t> off(cuts.begin(), cuts.end() - 1);
+      tile_concat_cols(pv, off, A.m, B.n, *C, cs);
+    }
+  });
+  return agree(g, rc);
 }
-
 
 // ---------------------------------------------------------------------------
 // SpParMat::Transpose (SpParMat.cpp:3528-3590) on a square grid: a diagonal
@@ -419,6 +765,7 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
 // world broadcasts, test only).  `out` is this rank's tile of the transpose.
 // ---------------------------------------------------------------------------
 int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
+  check_usable(g);
   if (g->pr != g->pc) return CBG_ERR_NOTSQUARE;
   hipStream_t cs = g->compute;
   // essentials of every rank's tile (world allgather: collective, diagonal ranks too)
@@ -441,7 +788,7 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
         if (bytes == 0) return;
         std::vector<char> h(bytes);
         if (mine) CBG_HIP(hipMemcpy(h.data(), src, bytes, hipMemcpyDeviceToHost));
-        host_check(g->hc.bcast(g->hc.user, COMM_WORLD, h.data(), bytes, q), "transpose bcast");
+        host_check(g, g->hc.bcast(g->hc.user, COMM_WORLD, h.data(), bytes, q), "transpose bcast");
         if (keep) CBG_HIP(hipMemcpy(dst, h.data(), bytes, hipMemcpyHostToDevice));
       };
       hb(R.cp, T.cp, sizeof(int64_t) * (qe[3] + 1));
@@ -465,7 +812,7 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
       CBG_NCCL(ncclRecv(R.val, pe[2], ncclFloat64, peer, c, g->comm));
     }
     CBG_NCCL(ncclGroupEnd());
-    CBG_HIP(hipStreamSynchronize(g->comm));
+    wait_comm(g);
   }
   if (diag) {
     tile_transpose(T, out, cs);
@@ -488,6 +835,7 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
 // ---------------------------------------------------------------------------
 int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, int dim, int64_t lo, int64_t hi,
                        cbg_tile& out) {
+  check_usable(g);
   if (dim != 0 && dim != 1) return CBG_ERR_INVALIDPARAMS;
   const int64_t gext = dim == 0 ? gm : gn;
   if (lo < 0 || hi < lo || hi > gext) return CBG_ERR_INVALIDPARAMS;
@@ -533,8 +881,9 @@ int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, i
     span(gext, np, q, Q0, Q1);
     const int64_t y0 = std::max(Q0, lo), y1 = std::max(y0, std::min(Q1, hi));  // slice of rank q
     cbg_tile sl = q == me ? mine : cbg_tile{};
-    bcast_tile(g, which, q, &E[4 * (size_t)q], sl, q == me);
-    CBG_HIP(hipStreamSynchronize(g->comm));
+    if (q != me) alloc_like(sl, &E[4 * (size_t)q]);
+    bcast_group(g, [&] { bcast_tile(g, which, q, &E[4 * (size_t)q], sl, q == me); });
+    wait_comm(g);
     const int64_t z0 = std::max(y0, T0), z1 = std::min(y1, T1);  // the part of it in my new range
     if (z1 > z0) {
       cbg_tile piece{};

@@ -61,17 +61,177 @@ void DevicePool::free(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(mu_);
   auto it = live_.find(p);
-  if (it == live_.end()) return;
+  if (it == live_.end()) {
+    auto g = grow_.find(p);
+    if (g != grow_.end()) {  // keep it mapped for the next growable request
+      in_use_ -= g->second.mapped;
+      cached_ += g->second.mapped;
+      grow_cache_.emplace(p, std::move(g->second));
+      grow_.erase(g);
+    }
+    return;
+  }
   free_.emplace(it->second, p);
   cached_ += it->second;
   in_use_ -= it->second;
   live_.erase(it);
 }
 
+// physical granule of the growable arrays (hipMemGetAllocationGranularity)
+static hipMemAllocationProp device_prop() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  return prop;
+}
+// Mapping sizes and offsets are multiples of 64 MiB: a multiple of the
+// recommended granularity and of the 2 MiB GPU page (a 545 MiB mapping after a
+// 256 MiB one made hipMemSetAccess fail with "invalid argument" on the box).
+static size_t granule() {
+  static thread_local size_t g = 0;
+  if (!g) {
+    hipMemAllocationProp prop = device_prop();
+    size_t rec = 0;
+    CBG_HIP(hipMemGetAllocationGranularity(&rec, &prop, hipMemAllocationGranularityRecommended));
+    g = (size_t)64 << 20;
+    while (rec > g) g <<= 1;
+  }
+  return g;
+}
+
+void* DevicePool::reserve_growable(size_t max_bytes) {
+  const size_t g = granule();
+  const size_t r = (std::max<size_t>(max_bytes, 1) + g - 1) / g * g;
+  {
+    // a cached block large enough, the most mapped first
+    std::lock_guard<std::mutex> lk(mu_);
+    auto best = grow_cache_.end();
+    for (auto it = grow_cache_.begin(); it != grow_cache_.end(); ++it)
+      if (it->second.reserved >= r && (best == grow_cache_.end() || it->second.mapped > best->second.mapped))
+        best = it;
+    if (best != grow_cache_.end()) {
+      void* p = best->first;
+      cached_ -= best->second.mapped;
+      in_use_ += best->second.mapped;
+      grow_.emplace(p, std::move(best->second));
+      grow_cache_.erase(best);
+      return p;
+    }
+  }
+  void* p = nullptr;
+  CBG_HIP(hipMemAddressReserve(&p, r, g, nullptr, 0));
+  std::lock_guard<std::mutex> lk(mu_);
+  grow_[p].reserved = r;
+  return p;
+}
+
+void DevicePool::grow(void* base, size_t bytes) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = grow_.find(base);
+  if (it == grow_.end()) throw HipError("grow: not a growable block", CBG_ERR_HIP);
+  Growable& gr = it->second;
+  if (bytes <= gr.mapped) return;
+  if (bytes > gr.reserved) throw HipError("growable block exhausted its reservation", CBG_ERR_OOM);
+  // map at least 256 MiB at a time (few mappings for tiles of 10^10 entries)
+  const size_t g = granule();
+  size_t step = std::max<size_t>(bytes - gr.mapped, (size_t)256 << 20);
+  step = std::min((step + g - 1) / g * g, gr.reserved - gr.mapped);
+  if (gr.mapped + step < bytes) step = (bytes - gr.mapped + g - 1) / g * g;
+  hipMemAllocationProp prop = device_prop();
+  hipMemGenericAllocationHandle_t h{};
+  hipError_t e = hipMemCreate(&h, step, &prop, 0);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    lk.unlock();
+    trim();  // drop the pool cache and retry once
+    lk.lock();
+    e = hipMemCreate(&h, step, &prop, 0);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      throw HipError("device allocation of " + std::to_string(step) + " bytes (growable) failed", CBG_ERR_OOM);
+    }
+  }
+  char* at = static_cast<char*>(base) + gr.mapped;
+  const char* what = "hipMemMap";
+  e = hipMemMap(at, step, 0, h, 0);
+  if (e == hipSuccess) {
+    hipMemAccessDesc d{};
+    d.location = prop.location;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    what = "hipMemSetAccess";
+    e = hipMemSetAccess(at, step, &d, 1);
+    if (e != hipSuccess) (void)hipMemUnmap(at, step);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipMemRelease(h);
+    size_t fr = 0, tot = 0;
+    (void)hipMemGetInfo(&fr, &tot);
+    throw HipError(std::string(what) + ": " + hipGetErrorString(e) + " (mapping " + std::to_string(step >> 20) +
+                       " MiB at offset " + std::to_string(gr.mapped >> 20) + " MiB of a " +
+                       std::to_string(gr.reserved >> 30) + " GiB range; device free " + std::to_string(fr >> 30) +
+                       " of " + std::to_string(tot >> 30) + " GiB)",
+                   CBG_ERR_OOM);
+  }
+  gr.chunks.emplace_back(h, step);
+  gr.mapped += step;
+  in_use_ += step;
+}
+
+void DevicePool::release_growable(void* base, Growable& gr) {
+  // callers free a tile only after the kernels that use it have completed.
+  // The physical pages go back to the driver, but the virtual range stays
+  // reserved for the life of the process: measured on the MI355X box, a range
+  // freed with hipMemAddressFree and handed out again (to a new growable block
+  // or to hipMalloc) read back stale or zero data in the next kernels
+  // (tests/test_multiprocess.py::test_fault_injection_gpu caught it); never
+  // reusing a virtual address avoids it, at no cost beyond address space.
+  (void)hipDeviceSynchronize();
+  size_t off = 0;
+  for (auto& c : gr.chunks) {
+    (void)hipMemUnmap(static_cast<char*>(base) + off, c.second);
+    (void)hipMemRelease(c.first);
+    off += c.second;
+  }
+  in_use_ -= gr.mapped;
+  gr.chunks.clear();
+  gr.mapped = 0;
+}
+
+// ----------------------------------------------------------------------------
+// EntryArena: C entries of consecutive multiplies, end to end
+// ----------------------------------------------------------------------------
+EntryArena::EntryArena() {
+  size_t fr = 0, tot = 0;
+  CBG_HIP(hipMemGetInfo(&fr, &tot));
+  // virtual reservations only: room for a tile filling the whole device
+  ir = static_cast<int32_t*>(pool().reserve_growable(tot / 2));
+  val = static_cast<double*>(pool().reserve_growable(tot));
+}
+EntryArena::~EntryArena() {
+  pool().free(ir);
+  pool().free(val);
+}
+void EntryArena::place(int64_t nnz, int32_t** pir, double** pval) {
+  pool().grow(ir, sizeof(int32_t) * (size_t)std::max<int64_t>(used + nnz, 1));
+  pool().grow(val, sizeof(double) * (size_t)std::max<int64_t>(used + nnz, 1));
+  *pir = ir + used;
+  *pval = val + used;
+  used += nnz;
+}
+
 void DevicePool::trim() {
   std::lock_guard<std::mutex> lk(mu_);
   for (auto& kv : free_) (void)hipFree(kv.second);
   free_.clear();
+  for (auto& kv : grow_cache_) {
+    in_use_ += kv.second.mapped;  // release_growable accounts it as in use
+    release_growable(kv.first, kv.second);
+  }
+  grow_cache_.clear();
   cached_ = 0;
 }
 
@@ -170,14 +330,26 @@ void tile_free_device(cbg_tile& t) {
   if (t.on_device) {
     pool().free(t.cp);
     pool().free(t.jc);
-    pool().free(t.ir);
-    pool().free(t.val);
+    if (!(t.reserved & TILE_BORROWED_ENTRIES)) {
+      pool().free(t.ir);
+      pool().free(t.val);
+    }
   }
   t.cp = nullptr;
   t.jc = nullptr;
   t.ir = nullptr;
   t.val = nullptr;
   t.nnz = t.nzc = 0;
+  t.reserved = 0;
+}
+
+TileGuard::~TileGuard() { tile_free_device(t); }
+TileGuard& TileGuard::operator=(TileGuard&& o) noexcept {
+  if (this != &o) {
+    tile_free_device(t);
+    t = o.release();
+  }
+  return *this;
 }
 
 // ----------------------------------------------------------------------------
@@ -236,8 +408,8 @@ __global__ void k_rowsplit_count(int64_t nzc, const int64_t* __restrict__ cp, co
                                  int64_t* __restrict__ fbot) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= nzc) return;
-  const int a = (int)cp[i], b = (int)cp[i + 1];
-  const int k = lower_bound_g(ir, a, b, cut) - a;
+  const int64_t a = cp[i], b = cp[i + 1];  // 64-bit: tiles may hold 2^31 or more entries
+  const int64_t k = lower_bound_g64(ir, a, b, cut) - a;
   ntop[i] = k;
   nbot[i] = (b - a) - k;
   ftop[i] = k > 0;
@@ -413,6 +585,130 @@ void tile_concat_rows(const std::vector<cbg_tile>& parts, const std::vector<int6
 }
 
 // ----------------------------------------------------------------------------
+// slices: columns [a, b) or rows [a, b) of a tile, re-based, one copy
+// (the stage pieces of the generalized SUMMA and the pipeline's B pieces)
+// ----------------------------------------------------------------------------
+void tile_slice_cols(const cbg_tile& T, int64_t a, int64_t b, cbg_tile& out, hipStream_t s) {
+  int64_t pos[2] = {0, 0}, cpos[2] = {0, 0};
+  if (T.nzc > 0) {
+    DBuf<int64_t> d(2);
+    hipLaunchKernelGGL(k_lower_bound_jc, dim3(1), dim3(1), 0, s, T.jc, T.nzc, a, d.p);
+    hipLaunchKernelGGL(k_lower_bound_jc, dim3(1), dim3(1), 0, s, T.jc, T.nzc, b, d.p + 1);
+    CBG_HIP(hipMemcpyAsync(pos, d.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipStreamSynchronize(s));
+    CBG_HIP(hipMemcpyAsync(&cpos[0], T.cp + pos[0], sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipMemcpyAsync(&cpos[1], T.cp + pos[1], sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipStreamSynchronize(s));
+  }
+  const int64_t nzc = pos[1] - pos[0], nnz = cpos[1] - cpos[0];
+  tile_alloc_device(out, T.m, b - a, nnz, nzc);
+  if (nzc > 0) {
+    hipLaunchKernelGGL(k_copy_cols, dim3((unsigned)((nzc + 256) / 256)), dim3(256), 0, s, nzc, T.jc + pos[0],
+                       T.cp + pos[0], a, cpos[0], out.jc, out.cp);
+    if (nnz) {
+      CBG_HIP(hipMemcpyAsync(out.ir, T.ir + cpos[0], sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, s));
+      CBG_HIP(hipMemcpyAsync(out.val, T.val + cpos[0], sizeof(double) * nnz, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  CBG_HIP(hipStreamSynchronize(s));
+}
+
+__global__ void k_rowslice_count(int64_t nzc, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir, int lo,
+                                 int hi, int64_t* __restrict__ first, int64_t* __restrict__ cnt,
+                                 int64_t* __restrict__ flag) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nzc) return;
+  const int64_t a = lower_bound_g64(ir, cp[i], cp[i + 1], lo);
+  const int64_t b = lower_bound_g64(ir, a, cp[i + 1], hi);
+  first[i] = a;
+  cnt[i] = b - a;
+  flag[i] = b > a;
+}
+__global__ void k_rowslice_copy(int64_t nzc, const int32_t* __restrict__ jc, const int32_t* __restrict__ ir,
+                                const double* __restrict__ val, int lo, const int64_t* __restrict__ first,
+                                const int64_t* __restrict__ off, const int64_t* __restrict__ col,
+                                int32_t* __restrict__ ojc, int64_t* __restrict__ ocp, int32_t* __restrict__ oir,
+                                double* __restrict__ oval) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  if (i >= nzc) return;
+  const int64_t k = off[i + 1] - off[i];
+  if (k == 0) return;
+  if (lane_id() == 0) {
+    ojc[col[i]] = jc[i];
+    ocp[col[i]] = off[i];
+  }
+  const int64_t a = first[i];
+  for (int64_t q = lane_id(); q < k; q += WAVE) {
+    oir[off[i] + q] = ir[a + q] - lo;
+    oval[off[i] + q] = val[a + q];
+  }
+}
+
+void tile_slice_rows(const cbg_tile& T, int64_t a, int64_t b, cbg_tile& out, hipStream_t s) {
+  const int64_t nz = T.nzc;
+  if (nz == 0) {
+    tile_alloc_device(out, b - a, T.n, 0, 0);
+    return;
+  }
+  DBuf<int64_t> first(nz + 1), cnt(nz + 1), flag(nz + 1), off(nz + 1), col(nz + 1);
+  hipLaunchKernelGGL(k_rowslice_count, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, nz, T.cp, T.ir, (int)a,
+                     (int)b, first.p, cnt.p, flag.p);
+  exclusive_scan_i64(cnt.p, off.p, nz, s);
+  exclusive_scan_i64(flag.p, col.p, nz, s);
+  int64_t h[2];
+  CBG_HIP(hipMemcpyAsync(&h[0], off.p + nz, 8, hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&h[1], col.p + nz, 8, hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  tile_alloc_device(out, b - a, T.n, h[0], h[1]);
+  hipLaunchKernelGGL(k_rowslice_copy, dim3((unsigned)((nz * WAVE + 255) / 256)), dim3(256), 0, s, nz, T.jc, T.ir,
+                     T.val, (int)a, first.p, off.p, col.p, out.jc, out.cp, out.ir, out.val);
+  CBG_HIP(hipMemcpyAsync(out.cp + h[1], &h[0], 8, hipMemcpyHostToDevice, s));
+  CBG_HIP(hipStreamSynchronize(s));
+}
+
+// ----------------------------------------------------------------------------
+// column assembly of arena-backed parts (no entry copies)
+// ----------------------------------------------------------------------------
+void tile_assemble_cols(const std::vector<cbg_tile>& parts, const std::vector<int64_t>& col_off, int64_t m, int64_t n,
+                        EntryArena& arena, cbg_tile& out, hipStream_t s) {
+  int64_t nnz = 0, nzc = 0;
+  for (size_t k = 0; k < parts.size(); ++k) {
+    if (parts[k].nnz > 0 && parts[k].ir != arena.ir + nnz)
+      throw HipError("tile_assemble_cols: parts are not laid out end to end in the arena", CBG_ERR_HIP);
+    nnz += parts[k].nnz;
+    nzc += parts[k].nzc;
+  }
+  if (nnz != arena.used) throw HipError("tile_assemble_cols: arena holds other entries", CBG_ERR_HIP);
+  out = cbg_tile{};
+  out.m = m;
+  out.n = n;
+  out.nnz = nnz;
+  out.nzc = nzc;
+  out.on_device = 1;
+  out.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzc + 1)));
+  out.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzc, 1)));
+  int64_t e = 0, c = 0;
+  for (size_t k = 0; k < parts.size(); ++k) {
+    const cbg_tile& p = parts[k];
+    if (p.nzc > 0)
+      hipLaunchKernelGGL(k_cat_cols, dim3((unsigned)((p.nzc + 255) / 256)), dim3(256), 0, s, p.nzc, p.jc, p.cp,
+                         col_off[k], e, out.jc + c, out.cp + c);
+    e += p.nnz;
+    c += p.nzc;
+  }
+  CBG_HIP(hipMemcpyAsync(out.cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  if (nnz > 0) {
+    out.ir = arena.ir;
+    out.val = arena.val;
+    arena.detach();
+  } else {
+    out.ir = static_cast<int32_t*>(pool().alloc(sizeof(int32_t)));
+    out.val = static_cast<double*>(pool().alloc(sizeof(double)));
+  }
+}
+
+// ----------------------------------------------------------------------------
 // digest (tests/golden/make_golden.py definition)
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
@@ -420,49 +716,66 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
   return z ^ (z >> 31);
 }
+// acc[2] counts order violations, as the reference driver's digest does: a
+// row id not strictly above its predecessor in the column, a column id not
+// strictly above the previous nonempty column, a decreasing or empty cp step
 __global__ void k_digest(int64_t nzc, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
                          const int32_t* __restrict__ ir, const double* __restrict__ val, int64_t roff, int64_t coff,
                          unsigned long long* __restrict__ acc, double* __restrict__ vsum) {
   const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
   if (i >= nzc) return;
   const unsigned long long col = (unsigned long long)(jc[i] + coff);
-  unsigned long long hs = 0, hv = 0;
+  const int64_t a = cp[i], b = cp[i + 1];
+  unsigned long long hs = 0, hv = 0, bad = 0;
   double vs = 0.0;
-  for (int64_t q = cp[i] + lane_id(); q < cp[i + 1]; q += WAVE) {
-    const unsigned long long h = mix64((col << 32) | (unsigned long long)(ir[q] + roff));
+  for (int64_t q = a + lane_id(); q < b; q += WAVE) {
+    const int r = ir[q];
+    const unsigned long long h = mix64((col << 32) | (unsigned long long)(r + roff));
     const double v = val[q];
     hs += h;
     hv += h * mix64(__double_as_longlong(v));
     vs += v;
+    if (q > a && ir[q - 1] >= r) ++bad;
+  }
+  if (lane_id() == 0) {
+    if (b <= a) ++bad;                     // DCSC columns are nonempty
+    if (i > 0 && jc[i - 1] >= jc[i]) ++bad;
   }
 #pragma unroll
   for (int d = WAVE / 2; d > 0; d >>= 1) {
     hs += __shfl_xor(hs, d, WAVE);
     hv += __shfl_xor(hv, d, WAVE);
     vs += __shfl_xor(vs, d, WAVE);
+    bad += __shfl_xor(bad, d, WAVE);
   }
   if (lane_id() == 0) {
     atomicAdd(&acc[0], hs);
     atomicAdd(&acc[1], hv);
+    if (bad) atomicAdd(&acc[2], bad);
     atomicAdd(vsum, vs);
   }
 }
 
 void tile_digest(const cbg_tile& t, int64_t roff, int64_t coff, uint64_t* hs, uint64_t* hv, double* vsum,
-                 hipStream_t s) {
-  DBuf<unsigned long long> acc(2);
+                 uint64_t* unsorted, hipStream_t s) {
+  DBuf<unsigned long long> acc(3);
   DBuf<double> vs(1);
-  CBG_HIP(hipMemsetAsync(acc.p, 0, 16, s));
+  CBG_HIP(hipMemsetAsync(acc.p, 0, 24, s));
   CBG_HIP(hipMemsetAsync(vs.p, 0, 8, s));
   if (t.nzc > 0)
     hipLaunchKernelGGL(k_digest, dim3((unsigned)((t.nzc * WAVE + 255) / 256)), dim3(256), 0, s, t.nzc, t.cp, t.jc, t.ir,
                        t.val, roff, coff, acc.p, vs.p);
-  unsigned long long h[2];
-  CBG_HIP(hipMemcpyAsync(h, acc.p, 16, hipMemcpyDeviceToHost, s));
+  unsigned long long h[3];
+  int64_t ends[2] = {0, 0};
+  CBG_HIP(hipMemcpyAsync(h, acc.p, 24, hipMemcpyDeviceToHost, s));
   CBG_HIP(hipMemcpyAsync(vsum, vs.p, 8, hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&ends[0], t.cp, 8, hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&ends[1], t.cp + t.nzc, 8, hipMemcpyDeviceToHost, s));
   CBG_HIP(hipStreamSynchronize(s));
   *hs = h[0];
   *hv = h[1];
+  // cp[0] == 0 and cp[nzc] == nnz close the chain of per-column checks
+  if (unsorted) *unsorted = h[2] + (ends[0] != 0) + (ends[1] != t.nnz);
 }
 
 // ---------------------------------------------------------------------------

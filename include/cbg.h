@@ -48,9 +48,12 @@ enum {
 };
 /* how the stages are executed on device (identical results up to fp order) */
 enum {
-  CBG_EXEC_PANEL = 0, /* gather the A block-row / B block-column panels, one local multiply, no merge */
-  CBG_EXEC_STAGED = 1 /* per-stage local multiply double-buffered against the next stage's broadcast,
-                         then an on-device multiway merge of the partial products */
+  CBG_EXEC_PANEL = 0, /* gather the A block-row, receive the B block-column in column pieces
+                         (piece p+1 broadcast while piece p multiplies), one local multiply per
+                         piece, C entries written end to end: no partial products, no merge */
+  CBG_EXEC_STAGED = 1 /* the reference's stages (any pr x pc grid: inner dimension cut at the union
+                         of A's column-block and B's row-block boundaries), stage s+1 broadcast while
+                         stage s multiplies, then an on-device multiway merge of the partials */
 };
 
 enum {
@@ -91,8 +94,12 @@ int cbg_tile_free(cbg_tile* t);
 int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* left, cbg_tile* right);
 /* row split of B as DoubleBuff does with Transpose/Split/Transpose (ParFriends.h:824-829), no transposes */
 int cbg_tile_split_rows(const cbg_tile* t, int64_t cut, cbg_tile* top, cbg_tile* bottom);
-/* structural + value digest (same definition as tests/golden/make_golden.py), device tile */
-int cbg_tile_digest(const cbg_tile* t, int64_t row_off, int64_t col_off, uint64_t* hs, uint64_t* hv, double* vsum);
+/* structural + value digest (same definition as tests/golden/make_golden.py), device tile.
+ * unsorted (may be NULL) receives the number of DCSC order violations: a row id not
+ * strictly above its predecessor in its column, a column id not strictly above the
+ * previous one, an empty column, cp[0] != 0 or cp[nzc] != nnz (0 for a valid tile). */
+int cbg_tile_digest(const cbg_tile* t, int64_t row_off, int64_t col_off, uint64_t* hs, uint64_t* hv, double* vsum,
+                    uint64_t* unsorted);
 /* SpDCCols::operator== (SpDCCols.h:74-81, Dcsc::operator== dcsc.cpp:472-510):
  * two empty tiles are equal; else m, n, nnz, nzc, cp, jc, ir must match and
  * values be ErrorTolerantEqual (Compare.h:47-65: equal, or absolute or
@@ -133,9 +140,13 @@ int cbg_local_symbolic(const cbg_tile* A, const cbg_tile* B, int64_t* flops, int
 /* MergeAll / MultiwayMerge (Friends.h:657-741, MultiwayMerge.h:409-526) of
  * column-sorted device tiles of equal shape, summing duplicates with SR::add. */
 int cbg_merge(const cbg_tile* parts, int nparts, int semiring, cbg_tile* C, void* hip_stream);
-/* last local multiply's statistics: flops, nnz, per-phase device ms, big columns, slabs */
+/* last call's local-multiply statistics (summed over its multiplies): flops, nnz,
+ * per-phase device ms, big columns, slabs.  Merges are not counted here. */
 int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms_numeric, int64_t* n_big,
                    int64_t* n_slabs);
+/* last call's multiway merges (MergeAll / MultiwayMerge): partial entries in,
+ * merged entries out, device ms */
+int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);
 
 /* ---------------- 2D SUMMA over RCCL ---------------- */
 typedef struct cbg_grid cbg_grid;
@@ -161,6 +172,15 @@ int cbg_grid_destroy(cbg_grid* g);
 int cbg_grid_info(const cbg_grid* g, int* rank, int* nranks, int* grid_rows, int* grid_cols, int* prow, int* pcol);
 /* world-communicator helpers used by drivers for barrier + max-over-ranks timing */
 int cbg_grid_barrier(cbg_grid* g);
+/* collective error agreement (no reference counterpart: the reference MPI_Aborts,
+ * SpDefs.h:69-76): *agreed = max over the grid's ranks of local_rc.  Every
+ * collective entry point below runs it after each of its steps, so a failure on
+ * one rank (CBG_ERR_OOM in its local multiply, a bad argument) is returned by
+ * every rank instead of leaving the others blocked in a broadcast.  An RCCL
+ * async error, or no progress for CBG_COMM_TIMEOUT_S seconds (default 600),
+ * aborts the grid's communicators (ncclCommAbort): later calls on that grid
+ * return CBG_ERR_RCCL. */
+int cbg_grid_agree(cbg_grid* g, int local_rc, int* agreed);
 int cbg_grid_allreduce_max(cbg_grid* g, double* value);
 int cbg_grid_allreduce_sum_i64(cbg_grid* g, int64_t* value);
 

@@ -16,6 +16,8 @@
 //   mult <algo> <sr> <A.cbgt> <B.cbgt> <out>  algo in {local, heap, doublebuff, synch}
 //                                            sr in {plus, minplus}; out=".cbgt" file
 //                                            or "-" for digest only
+//   multphased <algo> <sr> <A> <B> <phases>  B column pieces (SpDCCols::ColSplit), one
+//                                            Mult_AnXBn_<algo> per piece, C digested and freed
 //   symbolic <A.cbgt> <B.cbgt>               estimateFLOP + estimateNNZ_Hash totals
 //                                            (mtSpGEMM.h:1056,805)
 //   digest <file.cbgt>
@@ -248,6 +250,40 @@ int main(int argc, char* argv[]) {
       printf("{\"tag\": \"time_%s\", \"seconds\": %.6f, \"nprocs\": %d}\n", algo.c_str(), t1 - t0, nprocs);
     }
     if (std::string(argv[6]) != "-") write_tile(argv[6], C);
+  } else if (cmd == "multphased") {
+    // multphased <algo> <sr> <A.cbgt> <B.cbgt> <phases>  (1x1 grid): B cut into column
+    // pieces by the reference's SpDCCols::ColSplit, as MemEfficientSpGEMM does
+    // (ParFriends.h:552-553), each piece multiplied with Mult_AnXBn_<algo> and its C
+    // digested and freed before the next (C larger than host memory).  Prints the
+    // summed digest and the summed multiply time (the CPU baseline at scale 22).
+    std::string algo = argv[2], sr = argv[3];
+    const int phases = atoi(argv[6]);
+    if (nprocs != 1) { fprintf(stderr, "multphased: 1x1 only\n"); MPI_Abort(MPI_COMM_WORLD, 1); }
+    PMat* A = read_global_tile(argv[4], grid);
+    PMat* B = read_global_tile(argv[5], grid);
+    const int64_t n = B->getncol();
+    DCCols copyB = B->seq();
+    delete B;
+    std::vector<DCCols> pieces;
+    copyB.ColSplit(phases, pieces);
+    Digest tot;
+    double secs = 0;
+    for (int p = 0; p < (int)pieces.size(); ++p) {
+      PMat Bp(new DCCols(pieces[p]), grid);
+      pieces[p] = DCCols();
+      double t0 = MPI_Wtime();
+      PMat C = (sr == "minplus") ? run_mult<MP>(algo, *A, Bp) : run_mult<PT>(algo, *A, Bp);
+      secs += MPI_Wtime() - t0;
+      Digest d = tile_digest(C.seq(), 0, (int64_t)p * (n / phases));
+      tot.nnz += d.nnz; tot.nzc += d.nzc; tot.hs += d.hs; tot.hv += d.hv; tot.vsum += d.vsum;
+      tot.unsorted += d.unsorted;
+      printf("{\"tag\": \"phase\", \"phase\": %d, \"nnz\": %llu, \"seconds\": %.3f}\n", p,
+             (unsigned long long)d.nnz, secs);
+      fflush(stdout);
+    }
+    print_digest(("C_" + algo + "_" + sr).c_str(), tot);
+    printf("{\"tag\": \"time_%s\", \"seconds\": %.6f, \"nprocs\": %d, \"phases\": %d}\n", algo.c_str(), secs,
+           nprocs, phases);
   } else if (cmd == "symbolic") {
     PMat* A = read_global_tile(argv[2], grid);
     PMat* B = read_global_tile(argv[3], grid);

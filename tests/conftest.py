@@ -28,3 +28,16 @@ def load_cbg():
 @pytest.fixture(scope="session")
 def cbg():
     return load_cbg()
+
+
+@pytest.fixture(autouse=True)
+def _release_device_cache(request):
+    """after every GPU test: return libcbg's cached device memory to the driver, so
+    that the multi-process tests that follow (several processes on the one GPU)
+    find the HBM free (the scale-24 tile test alone caches hundreds of GB)"""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    mod = sys.modules.get("combblas_spmm_test_amd")
+    if mod is not None and getattr(mod, "_lib", None) is not None:
+        mod._lib.cbg_pool_trim()

@@ -29,6 +29,9 @@ def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     assert world == pr * pc
     port = int(os.environ["MASTER_PORT"]) + 1
+    if case == "fault" and rank == world - 1:
+        # its 2nd (PANEL) and 3rd (STAGED) SUMMA call, or the first two (CBG_FAULT_FIRST=1)
+        os.environ["CBG_FAULT_INJECT"] = "%d:%s" % (rank, "0,1" if os.environ.get("CBG_FAULT_FIRST") == "1" else "1,2")
     if mode == "gpu" or mode == "cputcp":
         # GPU processes never import torch (a second HIP runtime corrupts the heap)
         if mode == "gpu":
@@ -45,6 +48,96 @@ def main():
         dist.init_process_group("gloo")
         hc = cbg.GlooHostComm(pr, pc)
     G = golden()
+    if case == "agree":
+        # collective error agreement without a device: a code raised on one rank
+        # reaches every rank; then a rank that leaves makes its peers' next
+        # collective fail (CBG_ERR_RCCL) instead of hanging
+        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        ok = grid.agree(3102 if rank == world - 1 else 0) == 3102 and grid.agree(0) == 0
+        dist.barrier()
+        if rank == world - 1:
+            print("MPOK" if ok else "AGREE FAILED", flush=True)
+            os._exit(0)  # leave without a goodbye: the peers must not hang
+        try:
+            grid.agree(0)
+            ok = False
+        except cbg.CbgError as e:
+            ok = ok and e.code == 3101
+        print("MPOK" if ok else "PEER-LOSS NOT DETECTED", flush=True)
+        os._exit(0)
+    if case == "fault":
+        # CBG_FAULT_INJECT makes the last rank's first local multiply fail like
+        # an OOM: every rank must return 3102 (no hang), then the grid still works
+        Ah = load_npz("rmat_s10_ef16_A.npz")
+        gd = G["rmat"]["s10_ef16"]["C_local_plus"]
+        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        Ad = cbg.SpParMat.from_global(grid, Ah)
+        Bd = cbg.SpParMat.from_global(grid, Ah)
+        ok = True
+        r0, _ = cbg.block_range(Ah["m"], pr, grid.prow)
+        c0, _ = cbg.block_range(Ah["n"], pc, grid.pcol)
+        r1, _ = cbg.block_range(Ah["m"], pr, grid.prow)[1], 0
+        c1 = cbg.block_range(Ah["n"], pc, grid.pcol)[1]
+        Cg = load_npz("rmat_s10_ef16_C_local_plus.npz")
+        d0 = digest(cbg.sub_tile(Cg, r0, r1, c0, c1), r0, c0)  # this rank's tile of the golden C
+        first = os.environ.get("CBG_FAULT_FIRST") == "1"
+        if not first:
+            C0 = cbg.Mult_AnXBn_DoubleBuff(Ad, Bd, exec_mode=1)  # call 0: a good STAGED multiply
+            dd = C0.tile.digest(r0, c0)
+            if dd != d0:
+                print(rank, "first multiply differs", dd, d0, flush=True)
+            C0.tile.free()
+        for ex in (0, 1):
+            try:
+                cbg.Mult_AnXBn_DoubleBuff(Ad, Bd, exec_mode=ex)
+                ok = False
+                print(rank, "no error raised", flush=True)
+            except cbg.CbgError as e:
+                ok = ok and e.code == 3102
+                if e.code != 3102:
+                    print(rank, "wrong code", e, flush=True)
+        C = cbg.Mult_AnXBn_DoubleBuff(Ad, Bd)  # the next call succeeds on the same grid
+        d1 = C.tile.digest(r0, c0)
+        if d1 != d0:
+            print(rank, "final tile differs from the golden tile", d1, d0, flush=True)
+            ok = False
+        import pickle
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(C.tile.digest(r0, c0)))))]
+        tot = add_digests(alld)
+        ok = ok and tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and tot["hv"] == gd["hv"]
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if ok else f"FAULT TEST FAILED {tot}", flush=True)
+        return
+    if case == "rmat18":
+        # scale-18 R-MAT A*A on the grid, generated per tile on device: PANEL and
+        # STAGED (DoubleBuff + Synch) against the reference's digest, rows ordered
+        import pickle
+        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        Ad = cbg.SpParMat.rmat(grid, 18)
+        Bd = cbg.SpParMat.rmat(grid, 18)
+        gd = G["rmat"]["s18_ef16"]["C_local_plus"]
+        r0, _ = cbg.block_range(Ad.gm, pr, grid.prow)
+        c0, _ = cbg.block_range(Bd.gn, pc, grid.pcol)
+        ok = True
+        for algo, ex in (("doublebuff", 1), ("synch", 1), ("doublebuff", 0)):
+            f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
+            C = f(Ad, Bd, exec_mode=ex)
+            d = C.tile.digest(r0, c0)
+            C.tile.free()
+            alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(d))))]
+            tot = add_digests(alld)
+            uns = sum(x["unsorted"] for x in alld)
+            good = tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and tot["hv"] == gd["hv"] and uns == 0
+            if rank == 0:
+                print(algo, ex, "OK" if good else f"BAD {tot} unsorted={uns} vs {gd}", flush=True)
+            ok = ok and good
+        grid.destroy()
+        dist.barrier()
+        if rank == 0 and ok:
+            print("MPOK", flush=True)
+        return
     if case == "multtest":
         # ReleaseTests/MultTest.cpp SpGEMM part on a pr x pc grid: ParallelReadMM of
         # A, B, CControl; Synch / DoubleBuff / phased products == CControl
@@ -174,7 +267,7 @@ def main():
     Bd = cbg.SpParMat.from_global(grid, B)
     ok = True
     for algo in ("doublebuff", "synch"):
-        for ex in ((0, 1) if pr == pc else (0,)):
+        for ex in (0, 1):  # PANEL (pipelined) and STAGED (any grid shape)
             f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
             C = f(Ad, Bd, exec_mode=ex)
             r0, _ = cbg.block_range(A["m"], pr, grid.prow)
@@ -183,7 +276,7 @@ def main():
             import pickle
             alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(d))))]
             tot = add_digests(alld)
-            good = tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"]
+            good = tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and all(x["unsorted"] == 0 for x in alld)
             if case.startswith("rmat"):
                 good = good and tot["hv"] == gd["hv"]
             else:

@@ -35,8 +35,7 @@ def test_local_digest_vs_reference(cbg, scale):
     B = cbg.rmat_tile(scale, 16)
     C = cbg.LocalHybridSpGEMM(A, B)
     g = G["rmat"][f"s{scale}_ef16"]["C_local_plus"]
-    d = C.digest()
-    d["unsorted"] = 0
+    d = C.digest()  # `unsorted` counted on the device: 0 required
     assert_digest_eq(d, g)
     h = C.to_host()  # order: columns ascending, rows ascending inside each column
     assert np.all(np.diff(h["jc"]) > 0)
@@ -52,9 +51,7 @@ def test_minplus_digest(cbg, scale):
     A = cbg.rmat_tile(scale, 16)
     B = cbg.rmat_tile(scale, 16)
     C = cbg.LocalHybridSpGEMM(A, B, "minplus")
-    d = C.digest()
-    d["unsorted"] = 0
-    assert_digest_eq(d, G["rmat"][f"s{scale}_ef16"]["C_local_minplus"])
+    assert_digest_eq(C.digest(), G["rmat"][f"s{scale}_ef16"]["C_local_minplus"])
 
 
 @pytest.mark.parametrize("name", ["sevenvertex", "small_nonsym", "largeseq"])
@@ -259,16 +256,109 @@ def test_summa_single_rank(cbg, algo, exec_mode):
 @pytest.mark.parametrize("algo", ["doublebuff", "synch"])
 @pytest.mark.parametrize("exec_mode", [0, 1])
 def test_summa_rccl_single_rank(cbg, algo, exec_mode):
-    """The RCCL transport end to end on one GPU (1x1 grid: ncclCommInitRank, split, broadcasts)."""
+    """The RCCL transport end to end on one GPU (1x1 grid: ncclCommInitRank, ncclCommSplit,
+    and every collective of the path executed on one-rank communicators: the grouped
+    ncclBroadcast of the A/B tiles (PANEL) and of the stage pieces (STAGED), ncclAllGather
+    of the sizes, the agreement allgathers).  MemEfficientSpGEMM with 3 phases on PANEL
+    broadcasts B's column pieces one phase ahead and assembles C in the growable arena."""
     g = cbg.CommGrid(0, 1, unique_id=cbg.CommGrid.unique_id(), transport="rccl")
     A = cbg.SpParMat.rmat(g, 10)
     B = cbg.SpParMat.rmat(g, 10)
     f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
     C = f(A, B, exec_mode=exec_mode)
-    assert_tiles_equal(C.tile.to_host(), load_npz("rmat_s10_ef16_C_local_plus.npz"))
-    assert g.allreduce_max(3.5) == 3.5 and g.allreduce_sum(7) == 7
+    ref = load_npz("rmat_s10_ef16_C_local_plus.npz")
+    assert_tiles_equal(C.tile.to_host(), ref)
+    Cp = cbg.MemEfficientSpGEMM(A, B, 3, algo=cbg.DOUBLEBUFF if algo == "doublebuff" else cbg.SYNCH,
+                                exec_mode=exec_mode)
+    assert_tiles_equal(Cp.tile.to_host(), ref)
+    assert Cp.tile.digest()["unsorted"] == 0
+    assert g.allreduce_max(3.5) == 3.5 and g.allreduce_sum(7) == 7 and g.agree(0) == 0 and g.agree(5) == 5
+    T = A.copy()
+    T.Transpose()  # 1x1: the diagonal rank transposes locally
+    assert T.tile.nnz == A.tile.nnz
+    blk = A.BlockSplit(2, 1)  # BlockSplit's broadcasts over the one-rank column communicator
+    assert blk[0][0].tile.nnz + blk[1][0].tile.nnz == A.tile.nnz
     g.barrier()
     g.destroy()
+
+
+@pytest.mark.parametrize("chunk", ["20000", "3000"])
+def test_merge_int64_chunks(chunk):
+    """MergeAll over column chunks (the path of partials with 2^31 or more entries),
+    forced at small sizes by CBG_MERGE_CHUNK: merged tile == the one-product merge,
+    chunks laid end to end in the growable arena; merges stay out of last_stats()."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = """
+import json, sys
+sys.path.insert(0, %r)
+from conftest import load_cbg
+from helpers import load_npz
+cbg = load_cbg()
+A = cbg.Tile.from_dict(load_npz("rmat_s10_ef16_A.npz"))
+AA = cbg.LocalHybridSpGEMM(A, A)
+M = cbg.MergeAll([AA, A, A])  # three partials of one shape: A*A + 2A
+st, ms = cbg.last_stats(), cbg.merge_stats()
+h = M.to_host()
+print(json.dumps(dict(nnz=int(M.nnz), d=M.digest(), stats_nnz=st["nnz"], merge_in=ms["entries_in"],
+                      cp=h["cp"].tolist()[:50], ir=h["ir"].tolist()[:200], val=h["val"].tolist()[:200])))
+""" % os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    for env in ({}, {"CBG_MERGE_CHUNK": chunk}):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, **env))
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[bool(env)] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out[True] == out[False]
+    assert out[True]["d"]["unsorted"] == 0 and out[True]["stats_nnz"] == 0
+    assert out[True]["merge_in"] > out[True]["nnz"] > 0
+
+
+def _tile_totals(cbg, scale, pr, pc, phases):
+    """nnz of every rank's C tile of a pr x pc grid, computed on this one GPU the way
+    the rank computes it (its A block row times its B block column, generated on
+    device as the (pr x 1) / (1 x pc) tiles), streamed in B-column phases; returns
+    (total nnz, total order violations)."""
+    nv = 1 << scale
+    grid = _self_grid_1x1(cbg)
+    tot = bad = 0
+    for r in range(pr):
+        Ar = cbg.rmat_tile(scale, 16, grid=(pr, 1), pos=(r, 0))
+        for c in range(pc):
+            Bc = cbg.rmat_tile(scale, 16, grid=(1, pc), pos=(0, c))
+            A = cbg.SpParMat(Ar, grid, Ar.m, nv)
+            B = cbg.SpParMat(Bc, grid, nv, Bc.n)
+            seen = []
+
+            def consume(ph, off, t):
+                d = t.digest(0, off)
+                seen.append((d["nnz"], d["unsorted"]))
+
+            cbg.MemEfficientSpGEMM(A, B, phases, on_phase=consume)
+            tot += sum(x[0] for x in seen)
+            bad += sum(x[1] for x in seen)
+            Bc.free()
+        Ar.free()
+    grid.destroy()
+    return tot, bad
+
+
+def test_rank_tiles_scale22_2x2(cbg):
+    """Config 3's per-rank work on one GPU: the four C tiles of scale-22 A*A on a 2x2
+    grid (rank (r,c): A block row r times B block column c, 2 phases each); their
+    nonzeros add up to the reference's symbolic nnz(C) and every tile is row-sorted."""
+    tot, bad = _tile_totals(cbg, 22, 2, 2, 2)
+    assert tot == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"] and bad == 0
+
+
+def test_rank_tiles_scale24_2x4(cbg):
+    """Config 4's per-rank work on one GPU: the eight C tiles of scale-24 A*A on a 2x4
+    grid (about 2.3e10 nonzeros = 275 GB per tile: streamed in 4 B-column phases);
+    their nonzeros add up to the reference's symbolic nnz(C) = 183,028,712,946."""
+    tot, bad = _tile_totals(cbg, 24, 2, 4, 4)
+    assert tot == G["rmat"]["s24_ef16"]["symbolic"]["nnzC"] and bad == 0
 
 
 @pytest.mark.parametrize("env", [{"CBG_BITMAP_BUDGET_GB": "0"}, {"CBG_BIG_FLOPS": "64"},
@@ -630,6 +720,7 @@ def test_local_digest_large_vs_oracle(cbg, scale, sr):
     d = C.digest()
     C.free()
     assert d["nnz"] == g["nnz"] and d["nzc"] == g["nzc"] and d["hs"] == g["hs"] and d["hv"] == g["hv"], (d, g)
+    assert d["unsorted"] == 0  # rows strictly ascending in every column (Dcsc::operator== compares ir exactly)
     sym = G["rmat"].get(f"s{scale}_ef16", {}).get("symbolic")
     if sym:  # the reference's own symbolic total
         assert d["nnz"] == sym["nnzC"]
@@ -657,6 +748,7 @@ def test_phased_scale22_vs_oracle(cbg):
     B.tile.free()
     grid.destroy()
     assert (nnz, hs, hv) == (g["nnz"], g["hs"], g["hv"])
+    assert all(d["unsorted"] == 0 for d in parts)
     assert nnz == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"]
 
 

@@ -34,10 +34,10 @@ def free_port():
     raise RuntimeError("no free port pair")
 
 
-def launch(nproc, args, timeout=300):
+def launch(nproc, args, timeout=300, env=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(HERE, "mp_worker.py")] + args
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env or {}))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     return r.returncode, r.stdout + r.stderr
 
@@ -48,6 +48,36 @@ def launch(nproc, args, timeout=300):
 def test_host_transport_cpu(grid, case, transport):
     """gloo (GlooHostComm) and plain-TCP (TcpHostComm) transports: same collectives, same answers."""
     rc, out = launch(grid[0] * grid[1], [transport, str(grid[0]), str(grid[1]), case])
+    assert rc == 0 and "MPOK" in out, out[-3000:]
+
+
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2)])
+def test_error_agreement_cpu(grid):
+    """cbg_grid_agree over the TCP host transport without a device: one rank's code
+    reaches every rank, and a rank that disappears makes the others' next
+    collective return CBG_ERR_RCCL instead of hanging (the reference MPI_Aborts)."""
+    rc, out = launch(grid[0] * grid[1], ["cputcp", str(grid[0]), str(grid[1]), "agree"], timeout=120)
+    assert out.count("MPOK") == grid[0] * grid[1], out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("first", ["0", "1"])
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2), (2, 4)])
+def test_fault_injection_gpu(grid, first):
+    """An OOM-like failure in one rank's local multiply (CBG_FAULT_INJECT) is
+    returned by every rank for PANEL and STAGED; the grid then multiplies fine
+    (also when the failures are the grid's first calls)."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "fault"], timeout=300,
+                     env={"CBG_FAULT_FIRST": first})
+    assert rc == 0 and "MPOK" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(2, 2), (2, 4)])
+def test_summa_scale18_multiprocess_gpu(grid):
+    """Scale-18 A*A on 2x2 and 2x4 grids (tiles generated on device): STAGED DoubleBuff
+    and Synch (generalized stages on 2x4) and pipelined PANEL == the reference's digest."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "rmat18"], timeout=600)
     assert rc == 0 and "MPOK" in out, out[-3000:]
 
 
