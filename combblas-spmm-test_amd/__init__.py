@@ -70,7 +70,8 @@ EXPORTS = [
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
-    "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats",
+    "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
+    "cbg_tile_concat_cols", "cbg_device_memory",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -133,6 +134,9 @@ def lib():
         "cbg_grid_block_extract": ([vp, T, i64, i64, i32, i64, i64, T], i32),
         "cbg_grid_agree": ([vp, i32, ctypes.POINTER(i32)], i32),
         "cbg_merge_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double)], i32),
+        "cbg_tile_alloc": ([i64, i64, i64, i64, T], i32),
+        "cbg_tile_concat_cols": ([T, i32, T], i32),
+        "cbg_device_memory": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -231,6 +235,71 @@ class Tile:
         a, b = Tile(), Tile()
         _check(lib().cbg_tile_split_cols(ctypes.byref(self.c), cut, ctypes.byref(a.c), ctypes.byref(b.c)))
         return a, b
+
+    @staticmethod
+    def create(essentials):
+        """SpDCCols::Create(essentials) (SpDCCols.cpp:733-745): an uninitialised device tile
+        from GetEssentials() = [nnz, m, n, nzc] (a broadcast's receive buffer)."""
+        nnz, m, n, nzc = (int(x) for x in essentials)
+        t = Tile()
+        _check(lib().cbg_tile_alloc(m, n, nnz, nzc, ctypes.byref(t.c)))
+        return t
+
+    def GetEssentials(self):
+        """SpDCCols::GetEssentials (SpDCCols.cpp:786-795): [nnz, m, n, nzc]"""
+        return [int(self.c.nnz), int(self.c.m), int(self.c.n), int(self.c.nzc)]
+
+    def GetArrays(self):
+        """SpDCCols::GetArrays (SpDCCols.cpp:825-851): index arrays [cp, jc, ir] and value
+        arrays [numx] as (device address, element count, element bytes) -- the buffers a
+        broadcast of the tile moves (cp is int64 here, jc/ir int32)."""
+        c = self.c
+        if c.nnz == 0:
+            return dict(indarrs=[(None, 0, 8), (None, 0, 4), (None, 0, 4)], numarrs=[(None, 0, 8)])
+        return dict(indarrs=[(c.cp, c.nzc + 1, 8), (c.jc, c.nzc, 4), (c.ir, c.nnz, 4)],
+                    numarrs=[(c.val, c.nnz, 8)])
+
+    @staticmethod
+    def concat_cols(parts):
+        """SpDCCols::ColConcatenate / Merge: parts side by side (columns shifted)."""
+        arr = (CTile * len(parts))(*[p.c for p in parts])
+        t = Tile()
+        _check(lib().cbg_tile_concat_cols(arr, len(parts), ctypes.byref(t.c)))
+        return t
+
+    def Merge(self, a, b):
+        """SpDCCols::Merge (SpDCCols.cpp:1194-1223): self = [a | b]; a and b are released."""
+        t = Tile.concat_cols([a, b])
+        a.free()
+        b.free()
+        self.free()
+        self.c = t.c
+        t.c = CTile()
+
+    def Transpose(self):
+        """SpDCCols::Transpose (SpDCCols.cpp:853-873), in place."""
+        t = self.transpose()
+        self.free()
+        self.c = t.c
+        t.c = CTile()
+
+    def ColSplit(self, parts):
+        """SpDCCols::ColSplit (SpDCCols.cpp:936-970): `parts` column pieces cut at
+        (i+1)*(n/parts), the last taking the rest; this tile is released."""
+        w = self.n // parts
+        out, rest = [], self
+        for i in range(parts - 1):
+            left, right = rest.split_cols(w)
+            if rest is not self:
+                rest.free()
+            out.append(left)
+            rest = right
+        if rest is self:
+            rest, _ = self.split_cols(self.n)
+            _.free()
+        out.append(rest)
+        self.free()
+        return out
 
     def split_rows(self, cut):
         a, b = Tile(), Tile()
@@ -339,6 +408,13 @@ def device_count():
     c = ctypes.c_int()
     _check(lib().cbg_device_count(ctypes.byref(c)))
     return c.value
+
+
+def device_memory():
+    """(free, total) bytes of the device (hipMemGetInfo)."""
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(lib().cbg_device_memory(ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def pool_stats():

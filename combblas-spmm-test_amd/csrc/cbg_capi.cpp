@@ -161,6 +161,46 @@ int cbg_tile_free(cbg_tile* t) {
   });
 }
 
+int cbg_tile_alloc(int64_t m, int64_t n, int64_t nnz, int64_t nzc, cbg_tile* out) {
+  if (!out || m < 0 || n < 0 || nnz < 0 || nzc < 0 || nzc > n || (nzc == 0) != (nnz == 0))
+    return fail(CBG_ERR_INVALIDPARAMS, "bad tile sizes");
+  return guard([&] {
+    cbg_tile t{};
+    cbg::tile_alloc_device(t, m, n, nnz, nzc);
+    if (nzc > 0) CBG_HIP(hipMemset(t.cp, 0, sizeof(int64_t)));
+    *out = t;
+    return CBG_OK;
+  });
+}
+
+int cbg_tile_concat_cols(const cbg_tile* parts, int nparts, cbg_tile* out) {
+  if (!parts || nparts <= 0 || !out) return fail(CBG_ERR_INVALIDPARAMS, "no parts");
+  int64_t n = 0;
+  std::vector<int64_t> off;
+  for (int i = 0; i < nparts; ++i) {
+    if (int rc = check_tile(&parts[i], true, "part")) return rc;
+    if (parts[i].m != parts[0].m) return fail(CBG_ERR_DIMMISMATCH, "parts differ in row count");
+    off.push_back(n);
+    n += parts[i].n;
+  }
+  if (n >= INT32_MAX) return fail(CBG_ERR_INVALIDPARAMS, "local dimensions must fit int32");
+  return guard([&] {
+    std::vector<cbg_tile> v(parts, parts + nparts);
+    cbg::tile_concat_cols(v, off, parts[0].m, n, *out, default_stream());
+    return CBG_OK;
+  });
+}
+
+int cbg_device_memory(size_t* free_bytes, size_t* total_bytes) {
+  return guard([&] {
+    size_t f = 0, t = 0;
+    CBG_HIP(hipMemGetInfo(&f, &t));
+    if (free_bytes) *free_bytes = f;
+    if (total_bytes) *total_bytes = t;
+    return CBG_OK;
+  });
+}
+
 int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* l, cbg_tile* r) {
   if (int rc = check_tile(t, true, "tile")) return rc;
   if (cut < 0 || cut > t->n) return fail(CBG_ERR_INVALIDPARAMS, "cut out of range");

@@ -162,7 +162,10 @@ void DevicePool::grow(void* base, size_t bytes) {
     d.location = prop.location;
     d.flags = hipMemAccessFlagsProtReadWrite;
     what = "hipMemSetAccess";
-    e = hipMemSetAccess(at, step, &d, 1);
+    // access is set over the whole mapped range from the reservation's base
+    // (setting it on the new chunk alone failed with "invalid argument" on the box
+    // once other processes had used the device)
+    e = hipMemSetAccess(base, gr.mapped + step, &d, 1);
     if (e != hipSuccess) (void)hipMemUnmap(at, step);
   }
   if (e != hipSuccess) {

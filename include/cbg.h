@@ -90,6 +90,15 @@ int cbg_tile_upload(const cbg_tile* host, cbg_tile* dst);
 int cbg_tile_download(const cbg_tile* dev, cbg_tile* host);
 /* frees a device tile produced by libcbg (no-op for host tiles) */
 int cbg_tile_free(cbg_tile* t);
+/* SpDCCols::CreateImpl(essentials) (SpDCCols.cpp:733-745): an uninitialised device
+ * tile of the given sizes (cp[0] = 0), e.g. the receive buffers of BCastMatrix */
+int cbg_tile_alloc(int64_t m, int64_t n, int64_t nnz, int64_t nzc, cbg_tile* out);
+/* SpDCCols::ColConcatenate / Merge (SpDCCols.cpp:1194-1223, ParFriends.h:724-725):
+ * parts side by side (part k's columns shifted by the widths of parts 0..k-1),
+ * all with the same row count; device tiles */
+int cbg_tile_concat_cols(const cbg_tile* parts, int nparts, cbg_tile* out);
+/* device memory: free and total bytes (hipMemGetInfo) */
+int cbg_device_memory(size_t* free_bytes, size_t* total_bytes);
 /* SpDCCols::Split (SpDCCols.cpp:905-930): columns [0,cut) and [cut,n) (device) */
 int cbg_tile_split_cols(const cbg_tile* t, int64_t cut, cbg_tile* left, cbg_tile* right);
 /* row split of B as DoubleBuff does with Transpose/Split/Transpose (ParFriends.h:824-829), no transposes */
