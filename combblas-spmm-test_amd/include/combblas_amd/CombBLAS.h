@@ -6,7 +6,10 @@
 //   CommGrid(MPI_Comm,r,c)     CommGrid.h         CommGrid(MPI_Comm,r,c) -> RCCL grid
 //   SpParMat<IT,NT,DER>        SpParMat.h         SpParMat<IT,NT,DER>
 //   PlusTimesSRing/MinPlusSRing Semirings.h:212   PlusTimesSRing/MinPlusSRing
-//   LocalHybridSpGEMM          mtSpGEMM.h:212     LocalHybridSpGEMM  (returns a device SpDCCols*)
+//   LocalHybridSpGEMM          mtSpGEMM.h:212     LocalHybridSpGEMM  (returns SpTuples*, device entries)
+//   SpTuples<IT,NT>            SpTuples.h:65      SpTuples (col-major entries in HBM, host accessors)
+//   SpDCCols Create/GetArrays/ SpDCCols.cpp:733,   same names; GetArrays lists DEVICE addresses
+//     Transpose/Merge/ColSplit 825,853,1194,936
 //   LocalSpGEMM (heap)         mtSpGEMM.h:73      LocalSpGEMM (same kernel; summation order differs only)
 //   Mult_AnXBn_DoubleBuff      ParFriends.h:798   Mult_AnXBn_DoubleBuff
 //   Mult_AnXBn_Synch           ParFriends.h:1004  Mult_AnXBn_Synch
@@ -90,6 +93,32 @@ struct MinPlusSRing {
 };
 
 // ---------------------------------------------------------------- tiles
+// LocArr / Arr (LocArr.h:36-58): the arrays GetArrays() lists.  Here `addr` is a
+// DEVICE pointer (a broadcast buffer for RCCL, not for MPI) and, because the
+// tile's arrays have different widths (cp int64, jc/ir int32, numx f64),
+// every entry also carries its element size.
+template <class V, class C>
+struct LocArr {
+  LocArr() : addr(nullptr), count(0), elem_bytes(0) {}
+  LocArr(V* a, C c, size_t eb) : addr(a), count(c), elem_bytes(eb) {}
+  V* addr;
+  C count;
+  size_t elem_bytes;
+};
+template <class IT, class NT>
+struct Arr {
+  Arr(IT indsize, IT numsize) {
+    indarrs.resize(indsize);
+    numarrs.resize(numsize);
+  }
+  std::vector<LocArr<void, IT>> indarrs;  // cp (int64), jc (int32), ir (int32)
+  std::vector<LocArr<NT, IT>> numarrs;    // numx
+  IT totalsize() { return (IT)(indarrs.size() + numarrs.size()); }
+};
+
+template <class IT, class NT>
+class SpTuples;
+
 // SpDCCols<IT,NT>: a DCSC tile resident in HBM (int32 local indices, f64 values).
 template <class IT, class NT>
 class SpDCCols {
@@ -100,6 +129,10 @@ class SpDCCols {
 
   SpDCCols() { t_ = cbg_tile{}; }
   explicit SpDCCols(const cbg_tile& dev) : t_(dev) {}
+  // SpDCCols(const SpTuples&, bool transpose) (SpDCCols.cpp:108-190): the tuples
+  // (column-major, rows ascending) become this tile; a transposed view is built
+  // with Transpose() (SpTuples::SortRowBased + the transpose constructor)
+  SpDCCols(const SpTuples<IT, NT>& T, bool transpose);
   // from column-sorted host tuples (row, col, value), as SpDCCols(nRow,nCol,nTuples,tuples,false)
   SpDCCols(IT nRow, IT nCol, IT nTuples, const std::tuple<IT, IT, NT>* tuples, bool transpose = false) {
     if (transpose) throw std::invalid_argument("row-sorted input is not supported");
@@ -136,8 +169,95 @@ class SpDCCols {
     return eq != 0;
   }
   std::vector<IT> GetEssentials() const { return {(IT)t_.nnz, (IT)t_.m, (IT)t_.n, (IT)t_.nzc}; }
+  // SpDCCols::Create(essentials) / CreateImpl (SpDCCols.cpp:733-745): an
+  // uninitialised device tile {nnz, m, n, nzc} -- the receiving side of BCastMatrix
+  void Create(const std::vector<IT>& ess) {
+    if ((IT)ess.size() != esscount) cbg_abort_on(CBG_ERR_INVALIDPARAMS, "Create: esscount");
+    cbg_tile t{};
+    cbg_abort_on(cbg_tile_alloc((int64_t)ess[1], (int64_t)ess[2], (int64_t)ess[0], (int64_t)ess[3], &t), "Create");
+    reset(t);
+  }
+  // SpDCCols::GetArrays (SpDCCols.cpp:825-851): indarrs {cp[nzc+1], jc[nzc], ir[nnz]},
+  // numarrs {numx[nnz]}, device addresses (NULL / 0 for an empty tile)
+  Arr<IT, NT> GetArrays() const {
+    Arr<IT, NT> a(3, 1);
+    if (t_.nnz > 0) {
+      a.indarrs[0] = LocArr<void, IT>(t_.cp, (IT)(t_.nzc + 1), sizeof(int64_t));
+      a.indarrs[1] = LocArr<void, IT>(t_.jc, (IT)t_.nzc, sizeof(int32_t));
+      a.indarrs[2] = LocArr<void, IT>(t_.ir, (IT)t_.nnz, sizeof(int32_t));
+      a.numarrs[0] = LocArr<NT, IT>(reinterpret_cast<NT*>(t_.val), (IT)t_.nnz, sizeof(double));
+    } else {
+      a.indarrs[0] = LocArr<void, IT>(nullptr, 0, sizeof(int64_t));
+      a.indarrs[1] = LocArr<void, IT>(nullptr, 0, sizeof(int32_t));
+      a.indarrs[2] = LocArr<void, IT>(nullptr, 0, sizeof(int32_t));
+      a.numarrs[0] = LocArr<NT, IT>(nullptr, 0, sizeof(double));
+    }
+    return a;
+  }
+  // SpDCCols::Transpose (SpDCCols.cpp:853-873): in place
+  void Transpose() {
+    cbg_tile t{};
+    cbg_abort_on(cbg_tile_transpose(&t_, &t), "Transpose");
+    reset(t);
+  }
+  // SpDCCols::Merge (SpDCCols.cpp:1194-1223): *this = [partA | partB]; both are emptied
+  void Merge(SpDCCols& partA, SpDCCols& partB) {
+    cbg_tile parts[2] = {partA.t_, partB.t_}, t{};
+    cbg_abort_on(cbg_tile_concat_cols(parts, 2, &t), "Merge");
+    partA.reset(cbg_tile{});
+    partB.reset(cbg_tile{});
+    reset(t);
+  }
+  // SpDCCols::ColSplit (SpDCCols.cpp:936-970): `parts` pieces cut at
+  // (i+1)*(n/parts), the last taking the rest; destroys *this
+  void ColSplit(int parts, std::vector<SpDCCols>& matrices) {
+    const int64_t w = t_.n / parts;
+    matrices.clear();
+    matrices.reserve(parts);
+    cbg_tile rest = t_;
+    bool own_rest = false;
+    for (int i = 0; i + 1 < parts; ++i) {
+      cbg_tile l{}, r{};
+      cbg_abort_on(cbg_tile_split_cols(&rest, w, &l, &r), "ColSplit");
+      if (own_rest) cbg_tile_free(&rest);
+      matrices.emplace_back(l);
+      rest = r;
+      own_rest = true;
+    }
+    if (!own_rest) {  // one part: a copy
+      cbg_tile l{}, r{};
+      cbg_abort_on(cbg_tile_split_cols(&rest, t_.n, &l, &r), "ColSplit");
+      cbg_tile_free(&r);
+      rest = l;
+    }
+    matrices.emplace_back(rest);
+    reset(cbg_tile{});
+  }
+  // SpDCCols::ColConcatenate (ParFriends.h:724-725): the pieces side by side
+  void ColConcatenate(std::vector<SpDCCols>& matrices) {
+    std::vector<cbg_tile> v;
+    for (auto& m : matrices) v.push_back(m.t_);
+    cbg_tile t{};
+    cbg_abort_on(cbg_tile_concat_cols(v.data(), (int)v.size(), &t), "ColConcatenate");
+    for (auto& m : matrices) m.reset(cbg_tile{});
+    reset(t);
+  }
+  SpDCCols(SpDCCols&& o) noexcept : t_(o.t_) { o.t_ = cbg_tile{}; }
+  SpDCCols& operator=(SpDCCols&& o) noexcept {
+    if (this != &o) {
+      cbg_tile_free(&t_);
+      t_ = o.t_;
+      o.t_ = cbg_tile{};
+    }
+    return *this;
+  }
   const cbg_tile* tile() const { return &t_; }
   cbg_tile* tile() { return &t_; }
+  cbg_tile release() {
+    cbg_tile t = t_;
+    t_ = cbg_tile{};
+    return t;
+  }
 
   // SpDCCols::Split (SpDCCols.cpp:905-930): columns [0,n/2) and [n/2,n)
   void Split(SpDCCols& a, SpDCCols& b) {
@@ -164,6 +284,67 @@ class SpDCCols {
  private:
   cbg_tile t_;
 };
+
+// SpTuples<IT,NT> (SpTuples.h:65-297): the local multiply's output container.
+// The reference's is an AoS array of (row, col, value) tuples, column-major with
+// rows ascending; here the same entries stay on the device in that order, held
+// as the DCSC arrays the kernels emit (one device allocation, no AoS copy).
+// getnnz/getnrow/getncol, rowindex/colindex/numvalue(i) (host accessors, the
+// entries are fetched from HBM on first use), and SpDCCols(SpTuples, false)
+// mirror the reference's use in LocalHybridSpGEMM callers (ParFriends.h:888-896).
+template <class IT, class NT>
+class SpTuples {
+ public:
+  explicit SpTuples(const cbg_tile& t) : t_(t) {}
+  ~SpTuples() { cbg_tile_free(&t_); }
+  SpTuples(const SpTuples&) = delete;
+  SpTuples& operator=(const SpTuples&) = delete;
+  int64_t getnnz() const { return t_.nnz; }
+  IT getnrow() const { return (IT)t_.m; }
+  IT getncol() const { return (IT)t_.n; }
+  IT rowindex(int64_t i) const { return (IT)host().ir[i]; }
+  IT colindex(int64_t i) const { return (IT)host().col[i]; }
+  NT numvalue(int64_t i) const { return (NT)host().val[i]; }
+  const cbg_tile* tile() const { return &t_; }
+  cbg_tile release() {
+    cbg_tile t = t_;
+    t_ = cbg_tile{};
+    return t;
+  }
+
+ private:
+  struct Host {
+    std::vector<int32_t> ir, col;
+    std::vector<double> val;
+  };
+  const Host& host() const {
+    if (!h_) {
+      h_.reset(new Host());
+      std::vector<int64_t> cp(t_.nzc + 1);
+      std::vector<int32_t> jc(t_.nzc);
+      h_->ir.resize(t_.nnz);
+      h_->val.resize(t_.nnz);
+      cbg_tile h{0, 0, 0, 0, cp.data(), jc.data(), h_->ir.data(), h_->val.data(), 0, 0};
+      cbg_abort_on(cbg_tile_download(&t_, &h), "SpTuples");
+      h_->col.resize(t_.nnz);
+      for (int64_t i = 0; i < t_.nzc; ++i)
+        for (int64_t p = cp[i]; p < cp[i + 1]; ++p) h_->col[p] = jc[i];
+    }
+    return *h_;
+  }
+  cbg_tile t_;
+  mutable std::unique_ptr<Host> h_;
+};
+
+template <class IT, class NT>
+SpDCCols<IT, NT>::SpDCCols(const SpTuples<IT, NT>& T, bool transpose) {
+  cbg_tile c{}, r{};
+  // a device copy of the tuples' arrays (the reference copies the tuples too)
+  cbg_abort_on(cbg_tile_split_cols(T.tile(), T.tile()->n, &c, &r), "SpDCCols(SpTuples)");
+  cbg_tile_free(&r);
+  t_ = c;
+  if (transpose) Transpose();
+}
 
 // ---------------------------------------------------------------- grid
 class CommGrid {
@@ -452,19 +633,23 @@ class SpParMat {
 };
 
 // ---------------------------------------------------------------- products
+// LocalHybridSpGEMM (mtSpGEMM.h:213-217): the caller owns the returned
+// SpTuples* (delete it, or build an SpDCCols from it as ParFriends.h:888-896
+// does); clearA/clearB delete the inputs (mtSpGEMM.h:443-446)
 template <class SR, class NTO, class IT, class NT1, class NT2>
-SpDCCols<IT, NTO>* LocalHybridSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA,
-                                     bool clearB) {
+SpTuples<IT, NTO>* LocalHybridSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA, bool clearB,
+                                     IT* aux = nullptr) {
+  (void)aux;
   cbg_tile c{};
   cbg_abort_on(cbg_local_spgemm(A.tile(), B.tile(), SR::code, &c, nullptr), "LocalHybridSpGEMM");
   if (clearA) delete const_cast<SpDCCols<IT, NT1>*>(&A);
   if (clearB) delete const_cast<SpDCCols<IT, NT2>*>(&B);
-  return new SpDCCols<IT, NTO>(c);
+  return new SpTuples<IT, NTO>(c);
 }
 // LocalSpGEMM (heap kernel, mtSpGEMM.h:73-202): same C structure; the heap's
 // summation order only changes fp rounding, so it runs the same device kernel
 template <class SR, class NTO, class IT, class NT1, class NT2>
-SpDCCols<IT, NTO>* LocalSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
+SpTuples<IT, NTO>* LocalSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
   return LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB);
 }
 

@@ -16,7 +16,7 @@
 //   mult <algo> <sr> <A.cbgt> <B.cbgt> <out>  algo in {local, heap, doublebuff, synch}
 //                                            sr in {plus, minplus}; out=".cbgt" file
 //                                            or "-" for digest only
-//   multphased <algo> <sr> <A> <B> <phases>  B column pieces (SpDCCols::ColSplit), one
+//   multphased <algo> <sr> <A> <B> <phases> [first count]  B column pieces (SpDCCols::ColSplit), one
 //                                            Mult_AnXBn_<algo> per piece, C digested and freed
 //   symbolic <A.cbgt> <B.cbgt>               estimateFLOP + estimateNNZ_Hash totals
 //                                            (mtSpGEMM.h:1056,805)
@@ -256,8 +256,12 @@ int main(int argc, char* argv[]) {
     // (ParFriends.h:552-553), each piece multiplied with Mult_AnXBn_<algo> and its C
     // digested and freed before the next (C larger than host memory).  Prints the
     // summed digest and the summed multiply time (the CPU baseline at scale 22).
+    // optional [first count]: only phases first .. first+count-1 (one process per
+    // phase keeps the host's memory bounded: the reference's heap grows across calls)
     std::string algo = argv[2], sr = argv[3];
     const int phases = atoi(argv[6]);
+    const int first = argc > 7 ? atoi(argv[7]) : 0;
+    const int count = argc > 8 ? atoi(argv[8]) : phases;
     if (nprocs != 1) { fprintf(stderr, "multphased: 1x1 only\n"); MPI_Abort(MPI_COMM_WORLD, 1); }
     PMat* A = read_global_tile(argv[4], grid);
     PMat* B = read_global_tile(argv[5], grid);
@@ -269,6 +273,10 @@ int main(int argc, char* argv[]) {
     Digest tot;
     double secs = 0;
     for (int p = 0; p < (int)pieces.size(); ++p) {
+      if (p < first || p >= first + count) {
+        pieces[p] = DCCols();
+        continue;
+      }
       PMat Bp(new DCCols(pieces[p]), grid);
       pieces[p] = DCCols();
       double t0 = MPI_Wtime();

@@ -183,6 +183,17 @@ def main():
         ref = digest(oracle_local(transpose_host(Th), oracle_local(Ah, Th)))
         ok = ok and tot["nnz"] == ref["nnz"] and tot["hs"] == ref["hs"]
         ok = ok and abs(tot["vsum"] - ref["vsum"]) < 1e-9 * abs(ref["vsum"])
+        # min-plus S*A*T on the grid (config 5's semiring): exact, digest == oracle
+        mp = cbg.MinPlusSRing
+        SATm = cbg.PSpGEMM(S, cbg.PSpGEMM(A, T, mp), mp)
+        dm = SATm.tile.digest(r0, c0)
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(dm))))]
+        totm = add_digests(alld)
+        refm = digest(oracle_local(transpose_host(Th), oracle_local(Ah, Th, sr="minplus"), sr="minplus"))
+        okm = totm["nnz"] == refm["nnz"] and totm["hs"] == refm["hs"] and totm["hv"] == refm["hv"]
+        if not okm and rank == 0:
+            print("GALERKIN MINPLUS", totm, refm, flush=True)
+        ok = ok and okm
         grid.destroy()
         dist.barrier()
         if rank == 0:

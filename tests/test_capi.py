@@ -1,4 +1,5 @@
 """C-ABI boundary: libcbg.so loads and exports every entry point include/cbg.h declares (CPU-only)."""
+import pytest
 import ctypes
 import os
 import re
@@ -44,3 +45,21 @@ def test_block_range_matches_owner(cbg):
     # SpParMat::Owner: m_perproc = m / procrows, last block takes the remainder
     assert cbg.block_range(10, 3, 0) == (0, 3)
     assert cbg.block_range(10, 3, 2) == (6, 10)
+
+
+def test_reference_adapter_compiles():
+    """integration/ParFriends_cbg.h (the overloads a maintainer
+    adds next to ParFriends.h:798) compiles against the reference's own headers and
+    links with libcbg.so (integration/adapter_check.cpp; run on a GPU by
+    test_gpu_local.py::test_reference_adapter_runs)."""
+    import shutil
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.isdir("/root/reference") or not os.path.exists("/opt/conda/lib/libmpi.so"):
+        pytest.skip("needs the reference sources and MPICH (build container only)")
+    if shutil.which("make") is None:
+        pytest.skip("no make")
+    r = subprocess.run(["make", "-C", os.path.join(repo, "oracle"), "adapter"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert os.path.exists(os.path.join(repo, "oracle", "_ref", "adapter_check"))

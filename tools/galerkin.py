@@ -3,6 +3,7 @@
 
   python tools/galerkin.py [--scale S] [--order K] [--iters N] [--minplus]      (one rank: 1x1 grid)
   torchrun ... tools/galerkin.py --scale 22                                     (square grids: 4, 9, 16 ranks)
+  python tools/galerkin.py --scale 22 --minplus --rank-tiles 2x4               (per-rank work of a grid, one GPU)
 
 A = Graph500 R-MAT (loops removed, so A is its own off-diagonal part L) plus a
 seeded positive diagonal D (the driver's dvec); T = restriction operator
@@ -68,12 +69,69 @@ def grid_of(cbg):
         return cbg.CommGrid(rank, world, side, side, transport="host", host_comm=hc), rank, world
 
 
+def rank_tiles(cbg, a, A, T, S):
+    """Every rank's local work of the full restriction on a pr x pc grid, timed on this
+    one GPU: rank (r,c) multiplies A's block row r by T's block column c (AT(r,c)),
+    then S's block row r by AT's block column c (SAT(r,c)), as the PANEL SUMMA does
+    after its broadcasts (SpParMat::Owner blocks).  Communication is not included:
+    these are the per-GPU compute times of a pr x pc run."""
+    pr, pc = (int(x) for x in a.rank_tiles.lower().split("x"))
+
+    def rows(t, lo, hi):
+        top, bot = t.split_rows(hi)
+        bot.free()
+        _, mid = top.split_rows(lo)
+        _.free()
+        top.free()
+        return mid
+
+    def cols(t, lo, hi):
+        left, right = t.split_cols(hi)
+        right.free()
+        _, mid = left.split_cols(lo)
+        _.free()
+        left.free()
+        return mid
+
+    def run(sr):
+        per = []
+        for c in range(pc):
+            c0, c1 = cbg.block_range(T.gn, pc, c)
+            Tc = cols(T.tile, c0, c1)
+            ATc = cbg.LocalHybridSpGEMM(A.tile, Tc, sr)  # AT's block column c (all its rows)
+            for r in range(pr):
+                r0, r1 = cbg.block_range(A.gm, pr, r)
+                s0, s1 = cbg.block_range(S.gm, pr, r)
+                Ar, Sr = rows(A.tile, r0, r1), rows(S.tile, s0, s1)
+                cbg.synchronize()
+                t0 = time.perf_counter()
+                X = cbg.LocalHybridSpGEMM(Ar, Tc, sr)
+                Y = cbg.LocalHybridSpGEMM(Sr, ATc, sr)
+                cbg.synchronize()
+                per.append(dict(rank=[r, c], seconds=time.perf_counter() - t0, nnz_AT=X.nnz, nnz_SAT=Y.nnz))
+                for t in (X, Y, Ar, Sr):
+                    t.free()
+            ATc.free()
+            Tc.free()
+        return per
+
+    out = {"grid": "%dx%d" % (pr, pc), "note": "per-rank local products on one GPU, no communication"}
+    for name, sr in (("plus", cbg.PlusTimesSRing), ("minplus", cbg.MinPlusSRing)):
+        run(sr)  # warm-up
+        per = run(sr)
+        out[name] = {"max_rank_s": max(x["seconds"] for x in per), "mean_rank_s": sum(x["seconds"] for x in per) / len(per),
+                     "nnz_SAT": sum(x["nnz_SAT"] for x in per), "ranks": per}
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--scale", type=int, default=18)
     p.add_argument("--order", type=int, default=2)
     p.add_argument("--iters", type=int, default=3)
     p.add_argument("--minplus", action="store_true")
+    p.add_argument("--rank-tiles", default=None,
+                   help="RxC: time every rank's local products of a RxC grid on this one GPU (no communication)")
     a = p.parse_args()
     cbg = load()
     cbg.lib().cbg_set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, cbg.device_count()))
@@ -132,6 +190,8 @@ def main():
            "full_restriction_s": t_full, "split_restriction_s": t_split}
     if a.minplus:
         out["full_restriction_minplus_s"] = timed(lambda: full(cbg.MinPlusSRing))
+    if a.rank_tiles and world == 1:
+        out["rank_tiles"] = rank_tiles(cbg, a, A, T, S)
     if rank == 0:
         print(json.dumps(out), flush=True)
     grid.destroy()
