@@ -121,11 +121,15 @@ struct DBuf {
 // synchronized (buffers of kernels running on a side stream)
 struct DeferredFree {
   std::vector<void*> ptrs;
+  bool synced = false;  // set by the owner after its streams are synchronized
   template <class T>
   void take(DBuf<T>& b) {
     if (b.p) ptrs.push_back(b.detach());
   }
   ~DeferredFree() {
+    // an error path leaves without the owner's final sync: kernels may still
+    // use the buffers, so wait before they can be handed out again
+    if (!synced && !ptrs.empty()) (void)hipDeviceSynchronize();
     for (void* q : ptrs) pool().free(q);
   }
 };
@@ -161,9 +165,12 @@ struct APrepScope {
   ~APrepScope() { aprep_end(); }
 };
 
-// device exclusive scan of n int64 values -> out[0..n], returns nothing (total at out[n])
-void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s);
-void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s);
+// device exclusive scan of n int64 values -> out[0..n], returns nothing (total at out[n]).
+// df: the scan's temporaries are released with df (no host synchronization);
+// without it the scan synchronizes the stream before returning them.
+struct DeferredFree;
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df = nullptr);
+void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df = nullptr);
 
 // multiway merge of column-sorted partial tiles (cbg_merge.hip)
 // int64 entry counts: column chunks of < 2^30 stacked entries (CBG_MERGE_CHUNK

@@ -1708,30 +1708,42 @@ struct Binned {
   DBuf<int32_t> perm;
 };
 
-static void bin_columns(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr, int nthr,
-                        int64_t big, Binned& out, hipStream_t s) {
+// Binning in two halves so that the histogram's trip to the host rides on a
+// synchronization the caller makes anyway: bin_classify launches k_classify
+// and an async copy of the histogram; after the caller's next stream sync,
+// bin_scatter turns it into offsets and launches the scatter.
+struct BinPending {
   BinThr bt;
-  bt.nb = nthr + 1;
-  for (int i = 0; i < nthr; ++i) bt.t[i] = thr[i];
-  DBuf<uint8_t> bin(n);
-  DBuf<int> hist(2 * MAXBINS);
-  CBG_HIP(hipMemsetAsync(hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
-  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, big, bt, bin.p,
-                     hist.p);
-  std::vector<int> h(MAXBINS);
-  CBG_HIP(hipMemcpyAsync(h.data(), hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
-  CBG_HIP(hipStreamSynchronize(s));
-  out.count.assign(bt.nb, 0);
-  out.offset.assign(bt.nb + 1, 0);
-  for (int b = 0; b < bt.nb; ++b) {
-    out.count[b] = h[b];
-    out.offset[b + 1] = out.offset[b] + h[b];
+  DBuf<uint8_t> bin;
+  DBuf<int> hist;
+  std::vector<int> h;
+};
+static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
+                         int nthr, int64_t big, BinPending& bp, hipStream_t s) {
+  bp.bt.nb = nthr + 1;
+  for (int i = 0; i < nthr; ++i) bp.bt.t[i] = thr[i];
+  bp.bin.reset(n);
+  bp.hist.reset(2 * MAXBINS);
+  CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
+  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt, bp.bin.p,
+                     bp.hist.p);
+  bp.h.assign(MAXBINS, 0);
+  CBG_HIP(hipMemcpyAsync(bp.h.data(), bp.hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
+}
+static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, DeferredFree& df) {
+  const int nb = bp.bt.nb;
+  out.count.assign(nb, 0);
+  out.offset.assign(nb + 1, 0);
+  for (int b = 0; b < nb; ++b) {
+    out.count[b] = bp.h[b];
+    out.offset[b + 1] = out.offset[b] + bp.h[b];
   }
-  CBG_HIP(hipMemcpyAsync(hist.p + MAXBINS, out.offset.data(), sizeof(int) * bt.nb, hipMemcpyHostToDevice, s));
+  CBG_HIP(hipMemcpyAsync(bp.hist.p + MAXBINS, out.offset.data(), sizeof(int) * nb, hipMemcpyHostToDevice, s));
   out.perm.reset(n);
-  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, n, bin.p, bt.nb, hist.p + MAXBINS,
+  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, n, bp.bin.p, nb, bp.hist.p + MAXBINS,
                      out.perm.p);
-  CBG_HIP(hipStreamSynchronize(s));  // `bin`/`hist` are released on return
+  df.take(bp.bin);  // released after the multiply's final synchronization
+  df.take(bp.hist);
 }
 
 static int pick_panel_log(int64_t m) {
@@ -1907,7 +1919,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       const int64_t g = 1LL << (GROUP_LOG_MAX - c);
       thr[NSMALL + c] = (groups && g <= bp.R) ? gp * bp.R / g : -1;
     }
-    bin_columns(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sb, s);
+    BinPending sp;
+    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sp, s);
+    CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
+    bin_scatter(nz, sp, sb, s, df);
   }
   // small-column symbolic bins on the side stream, big columns on the main one
   fork(s);
@@ -1986,9 +2001,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     }
   }
   join(s);
-  // column pointers of C
+  // Everything that depends only on the per-column counts is launched now and
+  // read back in ONE synchronization: nnz(C) (column pointers), the number of
+  // slabs, the numeric bins' histogram and the number of nonempty C columns.
   DBuf<int64_t> colptr(nz + 1);
-  exclusive_scan_i32_to_i64(cnt.p, colptr.p, nz, s);
+  exclusive_scan_i32_to_i64(cnt.p, colptr.p, nz, s, &df);
   int64_t nnzc = 0;
   CBG_HIP(hipMemcpyAsync(&nnzc, colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   // slab lists of big columns
@@ -1997,11 +2014,26 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   int64_t nslabs = 0;
   if (nbig > 0) {
     sbase.reset(nbr + 1);
-    exclusive_scan_i32_to_i64(bp.nslab.p, sbase.p, nbr, s);
+    exclusive_scan_i32_to_i64(bp.nslab.p, sbase.p, nbr, s, &df);
     CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
+  BinPending npend;
+  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s);
+  // compaction of C's columns (SpDCCols(SpTuples): nonempty columns only)
+  DBuf<int64_t> flag(nz + 1), pos(nz + 1);
+  hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
+  exclusive_scan_i64(flag.p, pos.p, nz, s, &df);
+  int64_t nzcC = 0, flops_total = 0;
+  CBG_HIP(hipMemcpyAsync(&nzcC, pos.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&flops_total, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipEventRecord(ev1, s));
-  CBG_HIP(hipStreamSynchronize(s));
+  CBG_HIP(hipStreamSynchronize(s));  // host sync 2 of 4
+  C.nzc = nzcC;
+  C.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzcC + 1)));
+  C.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzcC, 1)));
+  Cg.t = C;
+  hipLaunchKernelGGL(k_col_scatter, dim3(nblk(nz + 1, 256)), dim3(256), 0, s, nz, cnt.p, pos.p, B.jc, colptr.p, C.jc,
+                     C.cp);
   int ncls[SLAB_NCLS] = {};
   if (nbig > 0 && nslabs > 0) {
     slist.reset(nslabs);
@@ -2016,7 +2048,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, counters.p + NK, slist.p, bp.perm_big, B.cp, colptr.p,
                        bp.gbm_slot.p, bp.plog, A.m);
     CBG_HIP(hipMemcpyAsync(ncls, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
-    CBG_HIP(hipStreamSynchronize(s));
+    CBG_HIP(hipStreamSynchronize(s));  // host sync 3 of 4: the slab classes' sizes
+    df.take(counters);
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
     {
@@ -2038,7 +2071,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   Cg.t = C;
   // numeric
   Binned nbn;
-  bin_columns(nz, flops.p, cnt.p, 1, kNumThr, 9, big, nbn, s);
+  bin_scatter(nz, npend, nbn, s, df);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
@@ -2048,21 +2081,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);
   }
   join(s);
-  // compaction of C's columns
-  DBuf<int64_t> flag(nz + 1), pos(nz + 1);
-  hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
-  exclusive_scan_i64(flag.p, pos.p, nz, s);
-  int64_t nzcC = 0;
-  CBG_HIP(hipMemcpyAsync(&nzcC, pos.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  CBG_HIP(hipStreamSynchronize(s));
-  C.nzc = nzcC;
-  C.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzcC + 1)));
-  C.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzcC, 1)));
-  Cg.t = C;
-  hipLaunchKernelGGL(k_col_scatter, dim3(nblk(nz + 1, 256)), dim3(256), 0, s, nz, cnt.p, pos.p, B.jc, colptr.p, C.jc,
-                     C.cp);
   CBG_HIP(hipEventRecord(ev2, s));
-  CBG_HIP(hipStreamSynchronize(s));
+  CBG_HIP(hipStreamSynchronize(s));  // host sync 4 of 4: C complete
+  df.synced = true;
   CBG_HIP(hipGetLastError());
   {
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
@@ -2100,9 +2121,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     st->nnz = nnzc;
     st->n_big = nbig;
     st->n_slabs = nslabs;
-    int64_t tot = 0;  // total flops (k_flops)
-    CBG_HIP(hipMemcpy(&tot, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost));
-    st->flops = tot;
+    st->flops = flops_total;  // total flops (k_flops), read back with sync 2
   }
   Cg.release();  // completed: the caller owns C
 }

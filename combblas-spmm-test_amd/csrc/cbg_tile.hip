@@ -290,7 +290,7 @@ __global__ void k_scan_add(int64_t* __restrict__ out, int64_t n, const int64_t* 
 }
 
 template <class TI>
-static void scan_impl(const TI* in, int64_t* out, int64_t n, hipStream_t s) {
+static void scan_impl(const TI* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df) {
   const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (nt <= 1) {
     if (n == 0) {
@@ -302,15 +302,22 @@ static void scan_impl(const TI* in, int64_t* out, int64_t n, hipStream_t s) {
   }
   DBuf<int64_t> sums(nt), offs(nt + 1);
   hipLaunchKernelGGL(k_scan_tile<TI>, dim3((unsigned)nt), dim3(SCAN_BS), 0, s, in, n, out, sums.p);
-  scan_impl<int64_t>(sums.p, offs.p, nt, s);
+  scan_impl<int64_t>(sums.p, offs.p, nt, s, df);
   hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, n, offs.p);
   CBG_HIP(hipMemcpyAsync(out + n, offs.p + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-  CBG_HIP(hipStreamSynchronize(s));  // sums/offs go back to the pool
+  if (df) {  // released when the caller's work on `s` has been synchronized
+    df->take(sums);
+    df->take(offs);
+  } else {
+    CBG_HIP(hipStreamSynchronize(s));  // sums/offs go back to the pool
+  }
 }
 
-void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s) { scan_impl<int64_t>(in, out, n, s); }
-void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s) {
-  scan_impl<int32_t>(in, out, n, s);
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df) {
+  scan_impl<int64_t>(in, out, n, s, df);
+}
+void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df) {
+  scan_impl<int32_t>(in, out, n, s, df);
 }
 
 // ----------------------------------------------------------------------------
