@@ -280,7 +280,7 @@ def main():
     peaks = [cbg.hbm_copy_bandwidth(4 << 30, 10) for _ in range(2)] if rank == 0 else []
     # K steps, each bracketed by barrier + synchronize and timed as the max over
     # ranks; the whole loop is bracketed the same way (the driver contract)
-    ms_local, step_s = [], []
+    ms_local, step_s, pipe = [], [], []
     grid.barrier()
     cbg.synchronize()
     t0 = time.perf_counter()
@@ -295,6 +295,7 @@ def main():
         st = cbg.last_stats()
         ms_local.append(st["ms_symbolic"] + st["ms_numeric"])
         step_s.append(te - ts)
+        pipe.append(cbg.summa_info())
     cbg.synchronize()
     grid.barrier()
     dt = time.perf_counter() - t0
@@ -341,6 +342,12 @@ def main():
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
                 "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport,
                 "phases": a.phases,
+                "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
+                                     "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],
+                                     "est_hidden_ms": [round(p_["est_hidden_ms"], 3) for p_ in pipe],
+                                     "rule": "B-column pieces broadcast one ahead when the measured first-piece "
+                                             "broadcast, scaled to the rest, exceeds the ~3 ms an extra piece costs"}
+                if N > 1 else None,
                 "C": "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer if stream_c
                      else "resident in HBM"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

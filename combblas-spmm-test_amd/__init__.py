@@ -71,7 +71,7 @@ EXPORTS = [
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
     "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
-    "cbg_tile_concat_cols", "cbg_device_memory",
+    "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -137,6 +137,8 @@ def lib():
         "cbg_tile_alloc": ([i64, i64, i64, i64, T], i32),
         "cbg_tile_concat_cols": ([T, i32, T], i32),
         "cbg_device_memory": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
+        "cbg_last_summa_info": ([ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_double)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -372,6 +374,14 @@ def last_stats():
                          ctypes.byref(ns))
     return dict(flops=f.value, nnz=n.value, ms_symbolic=a.value, ms_numeric=b.value, n_big=nb.value,
                 n_slabs=ns.value)
+
+
+def summa_info():
+    """the last PANEL SUMMA's double buffering: pieces multiplied, broadcast ms of the
+    first piece, estimated ms of the rest's broadcast (pipelined when worth an extra piece)."""
+    a, b, c = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+    lib().cbg_last_summa_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+    return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value)
 
 
 def merge_stats():

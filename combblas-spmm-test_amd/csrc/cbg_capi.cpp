@@ -479,6 +479,14 @@ int cbg_grid_agree(cbg_grid* g, int local_rc, int* agreed) {
   });
 }
 
+int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms) {
+  const cbg::SummaInfo& i = cbg::summa_info();
+  if (pieces) *pieces = i.pieces;
+  if (bcast_ms_piece0) *bcast_ms_piece0 = i.bcast_ms_piece0;
+  if (est_hidden_ms) *est_hidden_ms = i.est_hidden_ms;
+  return CBG_OK;
+}
+
 int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms) {
   const cbg::MergeStats& m = cbg::merge_stats();
   if (entries_in) *entries_in = m.entries_in;

@@ -154,6 +154,13 @@ struct MergeStats {
   double ms = 0;
 };
 MergeStats& merge_stats();
+// the last PANEL SUMMA's pipelining: pieces multiplied, measured broadcast
+// time of the first piece, and the transfer of the rest it estimated
+struct SummaInfo {
+  int pieces = 0;
+  double bcast_ms_piece0 = 0, est_hidden_ms = 0;
+};
+SummaInfo& summa_info();
 // A-side preparation (column maps of A) kept across the local multiplies of
 // one MemEfficientSpGEMM call, whose phases all multiply the same A: between
 // aprep_begin() and aprep_end() on a thread, a local multiply whose A has the

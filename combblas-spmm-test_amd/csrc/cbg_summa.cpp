@@ -69,6 +69,7 @@ struct cbg_grid {
   ncclComm_t world = nullptr, row = nullptr, col = nullptr;
   hipStream_t compute = nullptr, comm = nullptr;
   hipEvent_t ev_comm = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timing of the first piece's broadcast
   bool broken = false;  // communicators aborted: every later collective fails
   int64_t calls = 0;    // SUMMA calls made on this grid (fault-injection index)
   bool fault_armed = false;
@@ -88,6 +89,8 @@ void grid_setup_streams(cbg_grid* g) {
   CBG_HIP(hipStreamCreateWithFlags(&g->compute, hipStreamNonBlocking));
   CBG_HIP(hipStreamCreateWithFlags(&g->comm, hipStreamNonBlocking));
   CBG_HIP(hipEventCreateWithFlags(&g->ev_comm, hipEventDisableTiming));
+  CBG_HIP(hipEventCreate(&g->ev_t0));
+  CBG_HIP(hipEventCreate(&g->ev_t1));
 }
 
 int grid_shape(int nranks, int& rows, int& cols) {
@@ -145,6 +148,8 @@ void grid_destroy(cbg_grid* g) {
   if (g->compute) (void)hipStreamDestroy(g->compute);
   if (g->comm) (void)hipStreamDestroy(g->comm);
   if (g->ev_comm) (void)hipEventDestroy(g->ev_comm);
+  if (g->ev_t0) (void)hipEventDestroy(g->ev_t0);
+  if (g->ev_t1) (void)hipEventDestroy(g->ev_t1);
   delete g;
 }
 
@@ -390,9 +395,25 @@ static void alloc_like(cbg_tile& t, const int64_t e[4]) { tile_alloc_device(t, e
 // phases); else the pieces' entries go end to end into one EntryArena and C
 // is their column concatenation (ColConcatenate without a copy).
 // ---------------------------------------------------------------------------
+static int64_t tile_bytes(const int64_t e[4]) { return 8 * (e[3] + 1) + 4 * e[3] + 12 * e[2]; }
+
+SummaInfo& summa_info() {
+  static thread_local SummaInfo s;
+  return s;
+}
+
+// extra local multiply an additional pipeline piece costs (CBG_PIPELINE_MIN_MS):
+// measured 2.5-3.0 ms on scale-22 rank tiles of 2x2 and 4x2 grids (68-132 ms)
+static double pipeline_min_ms() {
+  static const char* e = getenv("CBG_PIPELINE_MIN_MS");
+  return e ? atof(e) : 3.0;
+}
+
 static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
-                       const std::vector<int64_t>& cuts, cbg_phase_fn fn, void* user, cbg_tile* C) {
-  const int np = (int)cuts.size() - 1;
+                       const std::vector<int64_t>& cuts_in, cbg_phase_fn fn, void* user, cbg_tile* C,
+                       bool adaptive = false) {
+  std::vector<int64_t> cuts = cuts_in;
+  int np = (int)cuts.size() - 1;
   const int pr = g->pr, pc = g->pc;
   hipStream_t cs = g->compute;
   // my B pieces (column slices; the whole tile when np == 1)
@@ -448,6 +469,10 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   if ((rc = agree(g, rc))) return rc;
   // from here on every rank has posted the same broadcasts: errors are
   // recorded, agreed on at the next step, and the comm stream is drained
+  SummaInfo& info = summa_info();
+  info = SummaInfo{};
+  info.pieces = np;
+  double host_ms0 = 0.0;
   int local = step([&] {
     bcast_group(g, [&] {
       for (int s = 0; s < pc; ++s) {
@@ -455,8 +480,68 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
         bcast_tile(g, COMM_ROW, s, &EA[4 * s], t, s == g->pcol);
       }
     });
+    CBG_HIP(hipEventRecord(g->ev_t0, g->comm));
+    const auto h0 = std::chrono::steady_clock::now();
     post_piece(0);
+    CBG_HIP(hipEventRecord(g->ev_t1, g->comm));
+    host_ms0 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
   });
+  // Adaptive double buffering (PANEL with the default two pieces on a grid):
+  // piece 0 (1/8 of B's columns) has been broadcast; its measured time, scaled
+  // to the rest's bytes, is the transfer that pipelining would hide behind
+  // piece 0's multiply.  An extra piece costs about pipeline_min_ms() of
+  // compute, so the ranks keep the two pieces only when the hidden transfer
+  // is larger (agreed over the grid: every rank cuts its B tile alike);
+  // otherwise the rest is broadcast at once and the pieces are rejoined into
+  // one multiply.
+  if (adaptive && np == 2 && !local) {
+    float ms0 = 0.f;
+    local = step([&] {
+      wait_comm(g);
+      if (g->host_mode) ms0 = (float)host_ms0;
+      else CBG_HIP(hipEventElapsedTime(&ms0, g->ev_t0, g->ev_t1));
+    });
+    int64_t b0 = 0, b1 = 0;
+    for (int s = 0; s < pr; ++s)
+      if (s != g->prow) {
+        b0 += tile_bytes(eB(s, 0));
+        b1 += tile_bytes(eB(s, 1));
+      }
+    const double hidden = b0 > 0 ? ms0 * (double)b1 / (double)b0 : 0.0;
+    info.bcast_ms_piece0 = ms0;
+    info.est_hidden_ms = hidden;
+    const int want = hidden > pipeline_min_ms() ? 1 : 0;
+    const int dec = agree(g, local ? local : want);  // codes >= 3001 are failures
+    if (dec > 1) {
+      rc = dec;
+    } else if (dec == 0) {
+      local = step([&] { alloc_piece(1); });
+      if (!(rc = agree(g, local))) {
+        local = step([&] {
+          post_piece(1);
+          wait_comm(g);  // the rest arrives now (its transfer is cheaper than a piece)
+          for (int s = 0; s < pr; ++s) {
+            const bool me = s == g->prow;
+            std::vector<cbg_tile> parts = {me ? piece[0] : Bc[0][s].t, me ? piece[1] : Bc[1][s].t};
+            TileGuard joined;
+            tile_concat_cols(parts, {0, cuts[1]}, eB(s, 0)[0], cuts[2], joined.t, cs);
+            if (me) {
+              own[0] = std::move(joined);
+              piece[0] = own[0].t;
+              tile_free_device(own[1].t);
+            } else {
+              Bc[0][s] = std::move(joined);
+              tile_free_device(Bc[1][s].t);
+            }
+          }
+          CBG_HIP(hipEventRecord(g->ev_comm, g->comm));
+        });
+        np = 1;
+        cuts = {0, cuts[2]};
+        info.pieces = 1;
+      }
+    }
+  }
   APrepScope aprep_scope;  // every piece multiplies the same A panel: keep its column maps
   std::unique_ptr<EntryArena> arena;
   if (!fn && np > 1) arena.reset(new EntryArena());
@@ -660,13 +745,20 @@ static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
 
 // pieces of the pipelined PANEL multiply when C stays resident: the first
 // piece small (its broadcast is exposed), the rest behind its multiply.
-// CBG_PIPELINE=k: k equal pieces (1 = no pipelining); default: 1 without
-// communication (one grid cell), else 2 with a first piece of 1/8 of B's columns
+// CBG_PIPELINE=k: k equal pieces (1 = no pipelining); CBG_PIPELINE=1/d: two
+// pieces, the first 1/d of B's columns; default: 1 piece without
+// communication (one grid cell), else 1/8
 static std::vector<int64_t> pipeline_cuts(cbg_grid* g, int64_t n) {
   static const char* e = getenv("CBG_PIPELINE");
-  int k = e ? atoi(e) : (g->pr * g->pc > 1 ? -2 : 1);
-  if (k == 0 || k == 1 || n < 16) return {0, n};
-  if (k == -2) return {0, n / 8, n};
+  const bool comm = g->pr * g->pc > 1;
+  if (n < 16) return {0, n};
+  if (!e) return comm ? std::vector<int64_t>{0, n / 8, n} : std::vector<int64_t>{0, n};
+  if (!strncmp(e, "1/", 2)) {
+    const int d = std::max(2, atoi(e + 2));
+    return {0, n / d, n};
+  }
+  int k = atoi(e);
+  if (k <= 1) return {0, n};
   k = (int)std::min<int64_t>(k, n);
   std::vector<int64_t> c;
   for (int i = 0; i <= k; ++i) c.push_back((int64_t)i * n / k);
@@ -687,7 +779,8 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
   if ((rc = agree(g, rc))) return rc;
   if (exec == CBG_EXEC_PANEL) {
     // every rank cuts its B tile at the same relative places (tiles of one grid column share n)
-    return summa_panel(g, A, B, A_gncol, B_gnrow, sr, pipeline_cuts(g, B.n), nullptr, nullptr, &C);
+    const bool adaptive = !getenv("CBG_PIPELINE") && g->pr * g->pc > 1;
+    return summa_panel(g, A, B, A_gncol, B_gnrow, sr, pipeline_cuts(g, B.n), nullptr, nullptr, &C, adaptive);
   }
   return summa_staged(g, A, B, A_gncol, B_gnrow, sr, algo, C);
 }
@@ -726,6 +819,7 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
       if ((rc = agree(g, rc))) return rc;
       Bu = &Bcopy.t;
     }
+    summa_info() = SummaInfo{};
     return summa_panel(g, A, *Bu, A_gncol, B_gnrow, sr, cuts, fn, user, C);
   }
   std::vector<TileGuard> parts;

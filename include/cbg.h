@@ -156,6 +156,11 @@ int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms
 /* last call's multiway merges (MergeAll / MultiwayMerge): partial entries in,
  * merged entries out, device ms */
 int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);
+/* last PANEL SUMMA call's double buffering: B-column pieces multiplied (1 = the
+ * broadcast was not pipelined), measured broadcast ms of the first piece, and
+ * the estimated broadcast ms of the rest that pipelining would hide (pipelined
+ * when it exceeds CBG_PIPELINE_MIN_MS, default 3: the cost of an extra piece) */
+int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms);
 
 /* ---------------- 2D SUMMA over RCCL ---------------- */
 typedef struct cbg_grid cbg_grid;

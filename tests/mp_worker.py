@@ -281,6 +281,8 @@ def main():
         for ex in (0, 1):  # PANEL (pipelined) and STAGED (any grid shape)
             f = cbg.Mult_AnXBn_DoubleBuff if algo == "doublebuff" else cbg.Mult_AnXBn_Synch
             C = f(Ad, Bd, exec_mode=ex)
+            if ex == 0 and rank == 0:
+                print("pieces %d" % cbg.summa_info()["pieces"], flush=True)
             r0, _ = cbg.block_range(A["m"], pr, grid.prow)
             c0, _ = cbg.block_range(B["n"], pc, grid.pcol)
             d = C.tile.digest(r0, c0)

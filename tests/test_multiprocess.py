@@ -85,6 +85,20 @@ def test_summa_scale18_multiprocess_gpu(grid):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("min_ms", ["0", "1e9"])
+@pytest.mark.parametrize("grid", [(2, 2), (4, 2)])
+def test_summa_pipeline_decision_gpu(grid, min_ms):
+    """The adaptive double buffering's two outcomes, forced: CBG_PIPELINE_MIN_MS=0 keeps
+    the two B-column pieces (piece 1 broadcast while piece 0 multiplies), 1e9 rejoins
+    them into one multiply after the rest's broadcast; both equal the reference."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "rmat"], timeout=600,
+                     env={"CBG_PIPELINE_MIN_MS": min_ms})
+    assert rc == 0 and "MPOK" in out, out[:1500] + out[-3000:]
+    want = "pieces 2" if min_ms == "0" else "pieces 1"
+    assert want in out, out[-2000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("grid", [(1, 2), (2, 1), (2, 2), (2, 4), (4, 2)])
 @pytest.mark.parametrize("case", ["rmat", "largeseq"])
 def test_summa_multiprocess_gpu(grid, case):

@@ -27,6 +27,9 @@ def main():
     p.add_argument("--ranks", default=None)
     p.add_argument("--reps", type=int, default=1)
     p.add_argument("--pieces", type=int, default=1, help="multiply B's tile in this many column pieces")
+    p.add_argument("--summa", action="store_true",
+                   help="run the rank's multiply through the PANEL SUMMA on a one-rank grid (the pipelined "
+                        "pieces of CBG_PIPELINE, the growable arena, A's maps kept across pieces)")
     a = p.parse_args()
     pr, pc = (int(x) for x in a.grid.split("x"))
     ranks = [int(x) for x in a.ranks.split(",")] if a.ranks else list(range(pr * pc))
@@ -37,6 +40,34 @@ def main():
         r, c = rk // pc, rk % pc
         Ap = cbg.rmat_tile(a.scale, a.ef, grid=(pr, 1), pos=(r, 0))
         Bp = cbg.rmat_tile(a.scale, a.ef, grid=(1, pc), pos=(0, c))
+        if a.summa:
+            class Self:
+                def bcast(self, comm, arr, root):
+                    pass
+
+                def allgather(self, comm, data):
+                    return data
+            g1 = cbg.CommGrid(0, 1, transport="host", host_comm=Self())
+            nv = 1 << a.scale
+            A1 = cbg.SpParMat(Ap, g1, Ap.m, nv)
+            B1 = cbg.SpParMat(Bp, g1, nv, Bp.n)
+            best = None
+            for _ in range(a.reps + 1):  # the first is a warm-up
+                cbg.synchronize()
+                t0 = time.perf_counter()
+                C = cbg.Mult_AnXBn_DoubleBuff(A1, B1)
+                cbg.synchronize()
+                dt = time.perf_counter() - t0
+                nnz = C.tile.nnz
+                C.tile.free()
+                best = dt if best is None or _ == 0 else min(best, dt)
+            print(json.dumps({"rank": rk, "grid": a.grid, "scale": a.scale, "s": best, "nnz_C": nnz,
+                              "nnzC_per_s": nnz / best, "pipeline": os.environ.get("CBG_PIPELINE", "default")}),
+                  flush=True)
+            g1.destroy()
+            Ap.free()
+            Bp.free()
+            continue
         pieces = []
         rest = Bp
         for q in range(a.pieces - 1):
