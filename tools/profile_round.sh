@@ -6,7 +6,7 @@
 # Raw outputs go to gpurun_out/prof_<tag>/; parse with tools/profile_collect.sh.
 set -e -o pipefail
 tag=$1; sc=${2:-18}; ph=${3:-1}
-out=gpurun_out/prof_$tag
+out=gpurun_out/prof_${tag}_s$sc
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/ks -o k -- python3 bench.py --scale $sc --phases $ph --steps ${STEPS:-10} --warmup 1 --no-cpu-baseline > $out/bench.json 2> $out/bench.err
