@@ -13,6 +13,39 @@ constexpr int WAVE = 64;
 #endif
 constexpr int EMPTY_KEY = 0x7FFFFFFF;  // empty hash slot; sorts after every row id
 
+// streaming stores/loads for data written or read once (C's entries, the kept
+// symbolic bitmaps): nontemporal, so they do not evict A's rows from L2
+#ifndef CBG_NT_OUT
+#define CBG_NT_OUT 1  // +2.8 % at scale 22, +6 % at 18 (same-box A/B)
+#endif
+#ifndef CBG_NT_EMIT
+#define CBG_NT_EMIT 1  // hash-slab emit stores too: +0.3 % at 22
+#endif
+template <class T>
+__device__ __forceinline__ void st_stream(T* p, T v) {
+#if CBG_NT_OUT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+#if CBG_NT_OUT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_emit(T* p, T v) {
+#if CBG_NT_EMIT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Order LDS traffic between the lanes of ONE wave (LDS executes a wave's
 // instructions in issue order; this stops the compiler from reordering).
 __device__ __forceinline__ void wave_sync() {
@@ -362,8 +395,8 @@ __device__ __forceinline__ void hash_emit_sorted(const int* keys, const double* 
     } else {
       for (int q = boff[b]; q < e; ++q) r += keys[members[q]] < k;
     }
-    out_ir[obase + r] = k;
-    out_val[obase + r] = vals[j];
+    st_emit(&out_ir[obase + r], k);
+    st_emit(&out_val[obase + r], vals[j]);
   }
 }
 

@@ -568,7 +568,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
         const int j = f * FW + q + lane;
         if (j < words) {
           const unsigned x = bm[j];
-          if (gdst) gdst[j] = x;
+          if (gdst) st_stream(&gdst[j], x);
           c += __popc(x);
         }
       }
@@ -970,8 +970,8 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
   const int64_t o = colptr[col];
   const int nout = (int)(colptr[col + 1] - o);
   for (int e = lane; e < nout; e += WAVE) {
-    out_ir[o + e] = keys[e];
-    out_val[o + e] = vals[e];
+    st_stream(&out_ir[o + e], keys[e]);
+    st_stream(&out_val[o + e], vals[e]);
   }
 }
 
@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #pragma unroll
     for (int k = 0; k < WPT; ++k) {
       const int j = k * BS + tid;
-      pw[k] = j < words ? src[j] : 0u;
+      pw[k] = j < words ? ld_stream(&src[j]) : 0u;
     }
   };
   auto fetch_stage1 = [&](const SlabRec& r) {
@@ -1267,7 +1267,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // values: coalesced copy; rows: each word scatters its set bits to their
     // ranks in LDS (reusing the value array), then a coalesced copy
     if (!(c_dbg & 8)) {
-      for (int j = tid; j < nout; j += BS) out_val[obase + j] = vals[j];
+      for (int j = tid; j < nout; j += BS) st_stream(&out_val[obase + j], vals[j]);
       __syncthreads();
       int* rows = reinterpret_cast<int*>(vals);
       for (int w = tid; w < words; w += BS) {
@@ -1279,7 +1279,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
       }
       __syncthreads();
-      for (int j = tid; j < nout; j += BS) out_ir[obase + j] = rows[j];
+      for (int j = tid; j < nout; j += BS) st_stream(&out_ir[obase + j], rows[j]);
     }
     __syncthreads();  // LDS is refilled by the next slab
     phase_mark(tmark, 6);
