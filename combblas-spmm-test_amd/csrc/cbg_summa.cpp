@@ -326,6 +326,9 @@ static int step(F&& f) {
   } catch (const std::bad_alloc&) {
     if (step_error().empty()) step_error() = "host allocation failed";
     return CBG_ERR_OOM;
+  } catch (const std::exception& e) {  // anything else still reaches the next agree()
+    if (step_error().empty()) step_error() = e.what();
+    return CBG_ERR_HIP;
   }
 }
 

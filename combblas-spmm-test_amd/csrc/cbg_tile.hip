@@ -211,8 +211,9 @@ EntryArena::EntryArena() {
   size_t fr = 0, tot = 0;
   CBG_HIP(hipMemGetInfo(&fr, &tot));
   // virtual reservations only: room for a tile filling the whole device
-  ir = static_cast<int32_t*>(pool().reserve_growable(tot / 2));
-  val = static_cast<double*>(pool().reserve_growable(tot));
+  // (12 bytes per entry: a third of the bytes for the row ids)
+  ir = static_cast<int32_t*>(pool().reserve_growable(tot / 3 + ((size_t)256 << 20)));
+  val = static_cast<double*>(pool().reserve_growable(2 * (tot / 3) + ((size_t)512 << 20)));
 }
 EntryArena::~EntryArena() {
   pool().free(ir);
