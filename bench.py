@@ -8,7 +8,7 @@ One step = one complete Mult_AnXBn_DoubleBuff (reference ParFriends.h:798-997)
 of Graph500 R-MAT A (SEED 0xDECAFBAD, ef 16, duplicates summed, loops removed)
 by a deep copy of A, inputs resident in HBM in the 2D block layout.  Every N
 runs the metric's scale 22.  N=1: C (297 GB) exceeds one GPU's HBM, so the
-multiply runs as MemEfficientSpGEMM with 4 B-column phases (ParFriends.h:449),
+multiply runs as MemEfficientSpGEMM with 3 B-column phases (ParFriends.h:449),
 each phase's C materialized in HBM and released; N>1: C left resident per
 tile.  N>1 is launched by torch.distributed.run, one rank per GPU, RCCL
 row/column communicators (grid 2x1, 2x2, 4x2 for 2/4/8).  --scale 18 gives
@@ -203,14 +203,14 @@ def main():
     scale = a.scale if a.scale is not None else 22
     if a.phases is None:
         # C streamed per B-column phase where a rank's C tile does not fit its
-        # HBM: scale 22 on one GPU (297 GB: 4 phases, measured within 0.5 % of
-        # 2 and 3), scale 24 on 8 (about 275 GB per rank); otherwise phases of
+        # HBM: scale 22 on one GPU (297 GB: 3 phases; 2 run out of HBM), scale
+        # 24 on 8 (about 275 GB per rank); otherwise phases of
         # at most ~80 GB of C (nnz(C) per scale from the reference's symbolic
         # totals, tests/golden/golden.json: s22 2.48e10, s24 1.83e11)
         nnz_est = {22: 2.48e10, 24: 1.83e11}.get(scale, 2.48e10 * 7.4 ** ((scale - 22) / 2.0))
         per_rank = 12.0 * nnz_est / N
         if N == 1 and scale == 22:
-            a.phases = 4
+            a.phases = 3  # 99 GB of C per phase; 3 vs 4 phases: 506-508 vs 509-511 ms (same box)
         else:
             a.phases = 1 if per_rank < 150e9 else int(-(-per_rank // 80e9))
     stream_c = a.phases > 1

@@ -202,8 +202,11 @@ __global__ __launch_bounds__(256) void k_copy16_nt(const uint4* __restrict__ src
 double hbm_copy_gbps(int64_t bytes, int reps) {
   const int64_t n = std::max<int64_t>(bytes / 16, 1);
   uint4 *a = nullptr, *b = nullptr;
-  CBG_HIP(hipMalloc(&a, n * 16));
-  CBG_HIP(hipMalloc(&b, n * 16));
+  // from the pool (no hipMalloc: after a large multiply the pool's cache may
+  // hold most of the device; pool().alloc drops the cache and retries)
+  DBuf<uint4> ba(n), bb(n);
+  a = ba.p;
+  b = bb.p;
   CBG_HIP(hipMemset(a, 1, n * 16));
   CBG_HIP(hipMemset(b, 0, n * 16));
   CBG_HIP(hipDeviceSynchronize());
@@ -234,9 +237,7 @@ double hbm_copy_gbps(int64_t bytes, int reps) {
   CBG_HIP(hipEventElapsedTime(&ms, e0, e1));
   CBG_HIP(hipEventDestroy(e0));
   CBG_HIP(hipEventDestroy(e1));
-  CBG_HIP(hipStreamDestroy(st));
-  CBG_HIP(hipFree(a));
-  CBG_HIP(hipFree(b));
+  CBG_HIP(hipStreamDestroy(st));  // (synchronized above: the pool may reuse a and b)
   return 2.0 * 16.0 * (double)n * reps / (ms * 1e-3) / 1e9;
 }
 
