@@ -206,10 +206,12 @@ def main():
         # HBM: scale 22 on one GPU (297 GB: 3 phases; 2 run out of HBM), scale
         # 24 on 8 (about 275 GB per rank); otherwise phases of
         # at most ~80 GB of C (nnz(C) per scale from the reference's symbolic
-        # totals, tests/golden/golden.json: s22 2.48e10, s24 1.83e11)
-        nnz_est = {22: 2.48e10, 24: 1.83e11}.get(scale, 2.48e10 * 7.4 ** ((scale - 22) / 2.0))
+        # totals, tests/golden/golden.json: s22 2.48e10, s24 1.83e11; s22 ef8
+        # 9.08e9 = 109 GB, resident on one GPU as SURVEY 8(d) asks)
+        nnz_est = {(22, 16): 2.48e10, (24, 16): 1.83e11, (22, 8): 9.08e9}.get(
+            (scale, a.ef), 2.48e10 * 7.4 ** ((scale - 22) / 2.0) * (a.ef / 16.0) ** 1.45)
         per_rank = 12.0 * nnz_est / N
-        if N == 1 and scale == 22:
+        if N == 1 and scale == 22 and a.ef == 16:
             a.phases = 3  # 99 GB of C per phase; 3 vs 4 phases: 506-508 vs 509-511 ms (same box)
         else:
             a.phases = 1 if per_rank < 150e9 else int(-(-per_rank // 80e9))

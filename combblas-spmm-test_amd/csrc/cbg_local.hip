@@ -1058,15 +1058,16 @@ constexpr int SLAB_SMALL_CAP = CBG_SLAB_SMALL_CAP, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
 // A's (row, value) of product position q
-template <int SR>
-__device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const double* __restrict__ valA, int q,
+// (VA = float: A's values narrowed losslessly, see k_vals_f32; the widening is exact)
+template <int SR, typename VA>
+__device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const VA* __restrict__ valA, int q,
                                            double b, int lo) {
-  return RowVal{irA[q] - lo, Sem<SR>::mul(valA[q], b)};
+  return RowVal{irA[q] - lo, Sem<SR>::mul((double)valA[q], b)};
 }
 
-template <int SR, int BS>
+template <int SR, int BS, typename VA>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
-                                              const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                              const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
   if (pass == 0) {
     block_products<BS>(
@@ -1086,12 +1087,12 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
   }
 }
 
-template <int SR, int CAP, int BS>
+template <int SR, int CAP, int BS, typename VA>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                  int64_t nA1, const int32_t* __restrict__ irA,
-                                                 const double* __restrict__ valA,
+                                                 const VA* __restrict__ valA,
                                                  int32_t* __restrict__ out_ir,
                                                  double* __restrict__ out_val, const unsigned* __restrict__ gbm) {
   // Persistent blocks (one per CU at this LDS size) pull slabs from a queue.
@@ -1258,7 +1259,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         } else {
           total = pref[BS];
         }
-        if (!(c_dbg & (2 << pass))) slab_products<SR, BS>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, VA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
       }
@@ -1312,12 +1313,12 @@ struct SlabHashLds {
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
-template <int SR, int TT, int BS, bool CMLEN>
+template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
 __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                       int64_t nA1, const int32_t* __restrict__ irA,
-                                                      const double* __restrict__ valA,
+                                                      const VA* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
   // persistent blocks over a queue of hash slabs; the next slab's record and
@@ -1417,7 +1418,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       if (c == nch - 1 && has_next) fetch1(nrec);
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
-          [&](const SegV& g, int u) { return a_rowval<SR>(irA, valA, g.off + u, g.b, 0); },
+          [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
           [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
       phase_mark(tmark, 14);
@@ -1598,6 +1599,7 @@ struct BigPlan {
   DBuf<int32_t> nslab, cnt_br;
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
+  const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
 };
 
 
@@ -1606,18 +1608,21 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
                              cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabHashLds<T, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, T, BS, false>;
-  set_lds(k, L);
-  static int per_cu = 0;
-  if (!per_cu) {
-    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-    if (per_cu < 1) per_cu = 1;
-  }
-  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                     A.n + 1, A.ir, A.val, C.ir, C.val);
+  auto go = [&](auto k, const auto* valA, int& per_cu) {
+    set_lds(k, L);
+    if (!per_cu) {
+      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+      if (per_cu < 1) per_cu = 1;
+    }
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
+                       A.n + 1, A.ir, valA, C.ir, C.val);
+  };
+  static int per_cu_d = 0, per_cu_f = 0;
+  if (bp.valAf) go(k_num_slab_hash<SR, T, BS, false, float>, bp.valAf, per_cu_f);
+  else go(k_num_slab_hash<SR, T, BS, false, double>, A.val, per_cu_d);
   df.take(queue);
 }
 
@@ -1626,18 +1631,21 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
                                cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabLds<CAP, BS>::BYTES;
-  auto k = k_num_slab<SR, CAP, BS>;
-  set_lds(k, L);
-  static int per_cu = 0;
-  if (!per_cu) {
-    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-    if (per_cu < 1) per_cu = 1;
-  }
-  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                     A.n + 1, A.ir, A.val, C.ir, C.val, bp.gbm.p);
+  auto go = [&](auto k, const auto* valA, int& per_cu) {
+    set_lds(k, L);
+    if (!per_cu) {
+      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+      if (per_cu < 1) per_cu = 1;
+    }
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
+                       A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p);
+  };
+  static int per_cu_d = 0, per_cu_f = 0;
+  if (bp.valAf) go(k_num_slab<SR, CAP, BS, float>, bp.valAf, per_cu_f);
+  else go(k_num_slab<SR, CAP, BS, double>, A.val, per_cu_d);
   df.take(queue);
 }
 
@@ -1788,7 +1796,28 @@ struct APrep {
   int64_t nnz = -1, nzc = -1, m = -1, n = -1;
   DBuf<int2> cmap, cmapP;  // cmapP: built by the first call that had big columns
   int plog = -1;
+  DBuf<float> valf;  // A's values as f32 (af == 1)
+  int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
+
+// A's values narrowed to f32, and whether every one survives the round trip
+// exactly (NaN and values outside f32's range or precision do not).  When they
+// all do, the slab kernels read 4 B per product instead of 8 and widen them:
+// the products and sums are the f64 ones, bit for bit.  CBG_AF32=0 disables.
+__global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __restrict__ f, int* __restrict__ inexact) {
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = v[i];
+    const float y = (float)x;
+    f[i] = y;
+    bad |= !((double)y == x);
+  }
+  if (bad) *inexact = 1;
+}
+static bool af32_enabled() {
+  static const char* e = getenv("CBG_AF32");
+  return !(e && !strcmp(e, "0"));
+}
 static APrep& aprep() {
   static thread_local APrep a;
   return a;
@@ -1798,6 +1827,8 @@ void aprep_end() {
   APrep& a = aprep();
   a.cmap.release();
   a.cmapP.release();
+  a.valf.release();
+  a.af = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
   a.nnz = a.nzc = a.m = a.n = -1;
@@ -1872,6 +1903,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (ap.active && !a_hit) {
     ap.cmap.release();
     ap.cmapP.release();
+    ap.valf.release();
+    ap.af = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
     ap.nnz = A.nnz;
@@ -1940,6 +1973,20 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
   const int nbig = bp.nbig;
   const int64_t nbr = (int64_t)nbig * bp.R;
+  // f32 copy of A's values for the slab kernels (checked once per A; the
+  // verdict is read back with host sync 2)
+  DBuf<float> valf_own;
+  DBuf<float>& valf = ap.active ? ap.valf : valf_own;
+  int af = ap.active ? ap.af : -1, af_inexact = 0;
+  DBuf<int> af_flag;
+  if (nbig > 0 && af < 0 && af32_enabled()) {
+    valf.reset(A.nnz);
+    af_flag.reset(1);
+    CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
+    const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
+    hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p);
+    CBG_HIP(hipMemcpyAsync(&af_inexact, af_flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+  }
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
     if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
@@ -2028,6 +2075,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipMemcpyAsync(&flops_total, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));  // host sync 2 of 4
+  if (af_flag.p) {
+    af = af_inexact ? 0 : 1;
+    if (ap.active) ap.af = af;
+    if (!af) valf.release();
+  }
+  if (af == 1) bp.valAf = valf.p;
   C.nzc = nzcC;
   C.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzcC + 1)));
   C.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzcC, 1)));

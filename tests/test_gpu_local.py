@@ -111,6 +111,34 @@ def test_big_columns_tall_matrix(cbg):
     assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh))
 
 
+@pytest.mark.parametrize("kind", ["f32_exact", "one_inexact", "out_of_f32_range"])
+def test_slab_value_narrowing(cbg, kind):
+    # slab kernels read A's values as f32 only when every one is exactly an f32
+    # (k_vals_f32); otherwise the f64 array: both must give the f64 products
+    rng = np.random.default_rng(11)
+    m, k, n = (1 << 19) + 5, 48, 6
+    nnz_per = 30000
+    rows = np.concatenate([np.sort(rng.choice(m, nnz_per, replace=False)) for _ in range(k)])
+    val = rng.choice(np.array([0.5, -2.25, 3.0, 1.0, -0.0, 1024.125]), len(rows))
+    if kind == "one_inexact":
+        val[12345] = 0.1
+    elif kind == "out_of_f32_range":
+        val[777] = 1e300
+        val[778] = 1e-300
+    Ah = dict(m=m, n=k, cp=np.arange(k + 1, dtype=np.int64) * nnz_per, jc=np.arange(k, dtype=np.int32),
+              ir=rows.astype(np.int32), val=val)
+    Bh = dict(m=k, n=n, cp=np.arange(n + 1, dtype=np.int64) * k, jc=np.arange(n, dtype=np.int32),
+              ir=np.tile(np.arange(k, dtype=np.int32), n), val=rng.uniform(-1, 1, n * k))
+    for sr in ("plus", "minplus"):
+        C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr)
+        assert cbg.last_stats()["n_big"] == n
+        ref = oracle_local(Ah, Bh, sr)
+        if sr == "plus":
+            assert_tiles_equal(C.to_host(), ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+        else:
+            assert_tiles_equal(C.to_host(), ref)
+
+
 def _panel_group_operands():
     """Tall A (m = 2^20 + 77: 5 row panels of 2^18, the last one partial) and a B whose
     columns land in every big-column class: panel groups of 4 and 2 (expected products

@@ -4,6 +4,7 @@ digest against the CPU oracle's (test infrastructure) for R-MAT `--scale`.
 
   python tools/check_scale.py --scale 20 [--sr minplus]      # local multiply
   python tools/check_scale.py --scale 22 --phases 4          # MemEfficientSpGEMM, digests streamed
+  python tools/check_scale.py --scale 22 --ef 8 --oracle-pieces 4   # one resident C on the GPU (109 GB)
 
 Digests (tests/helpers.py digest) add over column pieces, so the phased GPU
 run and the oracle (one B column piece at a time) are compared on the whole C
@@ -66,13 +67,18 @@ def main():
     p.add_argument("--threads", type=int, default=16)
     p.add_argument("--sr", choices=["plus", "minplus"], default="plus")
     p.add_argument("--phases", type=int, default=1)
+    p.add_argument("--ef", type=int, default=16)
+    p.add_argument("--oracle-pieces", type=int, default=None,
+                   help="B column pieces of the oracle run (default: --phases); bounds host memory")
     a = p.parse_args()
+    if a.oracle_pieces is None:
+        a.oracle_pieces = a.phases
     from conftest import load_cbg
     cbg = load_cbg()
     cbg.lib().cbg_set_device(0)
     t0 = time.time()
-    A = cbg.rmat_tile(a.scale, 16)
-    B = cbg.rmat_tile(a.scale, 16)
+    A = cbg.rmat_tile(a.scale, a.ef)
+    B = cbg.rmat_tile(a.scale, a.ef)
     if a.phases <= 1:
         C = cbg.LocalHybridSpGEMM(A, B, a.sr)
         gd = C.digest()
@@ -97,8 +103,8 @@ def main():
     print(json.dumps({"gpu": gd, "s": round(time.time() - t0, 1)}), flush=True)
     from helpers import oracle_local, oracle_rmat  # the checker
     t0 = time.time()
-    Ah = oracle_rmat(a.scale, 16, nthreads=a.threads)
-    if a.phases <= 1:
+    Ah = oracle_rmat(a.scale, a.ef, nthreads=a.threads)
+    if a.oracle_pieces <= 1:
         Ch = oracle_local(Ah, dict(Ah), a.sr, nthreads=a.threads)
         od = chunked_digest(Ch)
         del Ch
@@ -107,8 +113,9 @@ def main():
         sub_tile = cbg.sub_tile
         n = Ah["n"]
         parts = []
-        for ph in range(a.phases):
-            c0, c1 = ph * (n // a.phases), (n if ph == a.phases - 1 else (ph + 1) * (n // a.phases))
+        np_ = a.oracle_pieces
+        for ph in range(np_):
+            c0, c1 = ph * (n // np_), (n if ph == np_ - 1 else (ph + 1) * (n // np_))
             Ch = oracle_local(Ah, sub_tile(Ah, 0, Ah["m"], c0, c1), a.sr, nthreads=a.threads)
             parts.append(chunked_digest(Ch, c0))
             del Ch

@@ -1,6 +1,9 @@
+#!/bin/bash
+# per-phase block time of the slab kernels (CBG_DBG=16 wall-clock marks) at one scale:
+#   tools/gpu_phases.sh [scale] [phases]
 set -o pipefail
 mkdir -p gpurun_out
-for ph in 3 4 2; do
-  timeout -k 10 200 python bench.py --no-cpu-baseline --scale 22 --phases $ph > gpurun_out/ph_$ph.json 2>> gpurun_out/ph.err || exit 1
-  python3 -c "import json;d=json.load(open('gpurun_out/ph_$ph.json'));print('phases $ph', round(d['value']/1e9,2), 'G nnz/s', round(d['ms_per_step'],2), 'ms', round(d['roofline']['frac'],3))"
-done
+sc=${1:-22}; ph=${2:-3}
+CBG_DBG=16 timeout -k 10 300 python bench.py --no-cpu-baseline --scale $sc --phases $ph --steps 1 --warmup 1 \
+  > gpurun_out/phases_s$sc.json 2> gpurun_out/phases_s$sc.err || exit 1
+grep -E "cbg (phases|slabs)" gpurun_out/phases_s$sc.err | tail -8
