@@ -758,6 +758,27 @@ def test_local_digest_large_vs_oracle(cbg, scale, sr):
         assert d["nnz"] == sym["nnzC"]
 
 
+def test_local_scale22_ef8_resident(cbg):
+    """SURVEY 8(d)'s scale-22 ef8 case: one local multiply whose C (9.08 G nonzeros,
+    109 GB) stays resident on the GPU; its digest equals the oracle's
+    (tests/golden/oracle_large.json) and nnz the reference's symbolic total."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        g = json.load(f)["s22_ef8"]
+    A = cbg.rmat_tile(22, 8)
+    B = cbg.rmat_tile(22, 8)
+    assert A.nnz == G["rmat"]["s22_ef8"]["A"]["nnz"]
+    C = cbg.LocalHybridSpGEMM(A, B)
+    d = C.digest()
+    st = cbg.last_stats()
+    for t in (C, A, B):
+        t.free()
+    assert (d["nnz"], d["nzc"], d["hs"], d["hv"], d["unsorted"]) == (g["nnz"], g["nzc"], g["hs"], g["hv"], 0)
+    sym = G["rmat"]["s22_ef8"]["symbolic"]
+    assert d["nnz"] == sym["nnzC"] and st["flops"] == sym["flops"]
+
+
 @pytest.mark.parametrize("sr", ["plus", "minplus"])
 def test_phased_scale22_vs_oracle(cbg, sr):
     """The bench's configuration: R-MAT scale-22 A*A as MemEfficientSpGEMM with 4
