@@ -216,6 +216,14 @@ def main():
         else:
             a.phases = 1 if per_rank < 150e9 else int(-(-per_rank // 80e9))
     stream_c = a.phases > 1
+    rehearsal = N > 1 and os.environ.get("CBG_RANK_HOSTIDS") == "1"
+    if rehearsal:
+        # several ranks on ONE GPU (a development box): one NCCL_HOSTID per rank
+        # makes RCCL accept them (socket transport over loopback), so the N>1
+        # code path runs end to end; its times say nothing about xGMI
+        os.environ["NCCL_HOSTID"] = "cbg-bench-rank-%d" % rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     cbg = load_cbg()  # libcbg first: its HIP/RCCL runtimes are the ones the process uses
     cbg.lib().cbg_set_device(local_rank % max(1, cbg.device_count()))
 
@@ -244,7 +252,7 @@ def main():
         uid = hc.bcast_object(cbg.CommGrid.unique_id() if rank == 0 else None, root=0)
         try:
             grid = cbg.CommGrid(rank, N, pr, pc, unique_id=uid, transport="rccl")
-            transport = "rccl"
+            transport = "rccl (socket rehearsal: all ranks on one GPU)" if rehearsal else "rccl"
             hc.close()
         except cbg.CbgError as e:
             # e.g. several ranks on one GPU (RCCL rejects duplicate devices): keep

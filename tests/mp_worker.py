@@ -5,6 +5,14 @@ usage: mp_worker.py <mode> <grid_rows> <grid_cols> <case>
               shared GPU and checks the global digest against the reference's.
   mode "cpu": transport plumbing only (no device work): bcast/allgather through
               GlooHostComm and the block distribution of the golden matrix.
+  mode "rccl": as "gpu", but the grid's collectives run over RCCL with several
+              ranks.  The ranks share the one GPU of a development box, which
+              RCCL refuses for ranks it sees on one host ("Duplicate GPU"), so
+              every rank gets its own NCCL_HOSTID: RCCL then treats them as
+              separate hosts and moves data with its socket transport over
+              loopback.  Every RCCL call of the SUMMA (communicator split,
+              grouped broadcasts, send/recv of Transpose, allgathers, the error
+              agreement and abort) runs with more than one rank this way.
 """
 import os
 import sys
@@ -32,9 +40,13 @@ def main():
     if case == "fault" and rank == world - 1:
         # its 2nd (PANEL) and 3rd (STAGED) SUMMA call, or the first two (CBG_FAULT_FIRST=1)
         os.environ["CBG_FAULT_INJECT"] = "%d:%s" % (rank, "0,1" if os.environ.get("CBG_FAULT_FIRST") == "1" else "1,2")
-    if mode == "gpu" or mode == "cputcp":
+    if mode == "rccl":
+        os.environ["NCCL_HOSTID"] = "cbg-test-rank-%d" % rank
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    if mode in ("gpu", "cputcp", "rccl"):
         # GPU processes never import torch (a second HIP runtime corrupts the heap)
-        if mode == "gpu":
+        if mode != "cputcp":
             cbg.lib()
         hc = cbg.TcpHostComm(rank, world, pr, pc, "127.0.0.1", port)
 
@@ -48,11 +60,21 @@ def main():
         dist.init_process_group("gloo")
         hc = cbg.GlooHostComm(pr, pc)
     G = golden()
+
+    def make_grid():
+        if mode != "rccl":
+            return cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        uid = hc.bcast_object(cbg.CommGrid.unique_id() if rank == 0 else None, root=0)
+        g = cbg.CommGrid(rank, world, pr, pc, unique_id=uid, transport="rccl")
+        if rank == 0:
+            print("transport rccl, %d ranks" % world, flush=True)
+        return g
+
     if case == "agree":
         # collective error agreement without a device: a code raised on one rank
         # reaches every rank; then a rank that leaves makes its peers' next
         # collective fail (CBG_ERR_RCCL) instead of hanging
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         ok = grid.agree(3102 if rank == world - 1 else 0) == 3102 and grid.agree(0) == 0
         dist.barrier()
         if rank == world - 1:
@@ -70,7 +92,7 @@ def main():
         # an OOM: every rank must return 3102 (no hang), then the grid still works
         Ah = load_npz("rmat_s10_ef16_A.npz")
         gd = G["rmat"]["s10_ef16"]["C_local_plus"]
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         Ad = cbg.SpParMat.from_global(grid, Ah)
         Bd = cbg.SpParMat.from_global(grid, Ah)
         ok = True
@@ -114,7 +136,7 @@ def main():
         # scale-18 R-MAT A*A on the grid, generated per tile on device: PANEL and
         # STAGED (DoubleBuff + Synch) against the reference's digest, rows ordered
         import pickle
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         Ad = cbg.SpParMat.rmat(grid, 18)
         Bd = cbg.SpParMat.rmat(grid, 18)
         gd = G["rmat"]["s18_ef16"]["C_local_plus"]
@@ -141,7 +163,7 @@ def main():
     if case == "multtest":
         # ReleaseTests/MultTest.cpp SpGEMM part on a pr x pc grid: ParallelReadMM of
         # A, B, CControl; Synch / DoubleBuff / phased products == CControl
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         mm = os.path.join(HERE, "golden", "sevenvertex.mtx")
         A = cbg.SpParMat.ParallelReadMM(grid, mm)
         B = cbg.SpParMat.ParallelReadMM(grid, mm)
@@ -158,7 +180,7 @@ def main():
         # exchange), PSpGEMMs, DimApply, +=, operator==; SAT digest vs the oracle
         from helpers import add_diag_host, oracle_local, restriction_host, transpose_host
         import pickle
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         scale, n = 10, 1 << 10
         dv = np.random.default_rng(7).uniform(0.5, 1.5, n)
         Lh = load_npz("rmat_s10_ef16_A.npz")
@@ -204,7 +226,7 @@ def main():
         # every block over the whole grid (standard layout), the C blocks at their
         # offsets add up to the golden A*A digest
         import pickle
-        grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+        grid = make_grid()
         Ah = load_npz("rmat_s10_ef16_A.npz")
         A = cbg.SpParMat.from_global(grid, Ah)
         B = cbg.SpParMat.from_global(grid, Ah)
@@ -273,7 +295,7 @@ def main():
         if rank == 0:
             print("MPOK", flush=True)
         return
-    grid = cbg.CommGrid(rank, world, pr, pc, transport="host", host_comm=hc)
+    grid = make_grid()
     Ad = cbg.SpParMat.from_global(grid, A)
     Bd = cbg.SpParMat.from_global(grid, B)
     ok = True

@@ -4,7 +4,9 @@ CPU (gloo, no device work): the host transport's row/column broadcasts and
 allgathers and the SpParMat::Owner block distribution.
 GPU: the full SUMMA (panel + staged, DoubleBuff + Synch) with several ranks
 sharing one GPU through the same transport, checked against the reference's
-global digest (the digest is additive over tiles)."""
+global digest (the digest is additive over tiles); and the same over RCCL
+communicators of several ranks (one NCCL_HOSTID per rank: RCCL's socket
+transport, since RCCL refuses ranks of one host on one GPU)."""
 import os
 import socket
 import subprocess
@@ -129,3 +131,15 @@ def test_blockspgemm_multiprocess_gpu(grid):
     the block products, checked against the golden A*A digest (host transport)."""
     rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "blockspgemm"], timeout=600)
     assert rc == 0 and "MPOK" in out, out[:1500] + out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid,case", [((1, 2), "rmat"), ((2, 2), "rmat"), ((2, 4), "largeseq"), ((2, 2), "galerkin"),
+                                       ((2, 2), "fault"), ((2, 2), "rmat18")])
+def test_rccl_multirank_gpu(grid, case):
+    """RCCL with several ranks (mp_worker mode "rccl": one NCCL_HOSTID per rank, so the
+    ranks sharing this GPU talk through RCCL's socket transport): the PANEL pipeline
+    and STAGED SUMMA, phases, Transpose's send/recv and the error agreement on real
+    RCCL communicators, against the same golden digests as the host transport."""
+    rc, out = launch(grid[0] * grid[1], ["rccl", str(grid[0]), str(grid[1]), case], timeout=300)
+    assert rc == 0 and "MPOK" in out and "transport rccl" in out, out[:1500] + out[-3000:]
