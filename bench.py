@@ -363,8 +363,10 @@ def main():
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
                                      "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],
                                      "est_hidden_ms": [round(p_["est_hidden_ms"], 3) for p_ in pipe],
+                                     "piece_cost_ms": [round(p_["piece_cost_ms"], 3) for p_ in pipe],
                                      "rule": "B-column pieces broadcast one ahead when the measured first-piece "
-                                             "broadcast, scaled to the rest, exceeds the ~3 ms an extra piece costs"}
+                                             "broadcast, scaled to the rest, exceeds what an extra piece costs: "
+                                             "max(3 ms, 4 % of the previous step's local multiply)"}
                 if N > 1 else None,
                 "C": "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer if stream_c
                      else "resident in HBM"},

@@ -138,7 +138,7 @@ def lib():
         "cbg_tile_concat_cols": ([T, i32, T], i32),
         "cbg_device_memory": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
         "cbg_last_summa_info": ([ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
-                                 ctypes.POINTER(ctypes.c_double)], i32),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -378,10 +378,11 @@ def last_stats():
 
 def summa_info():
     """the last PANEL SUMMA's double buffering: pieces multiplied, broadcast ms of the
-    first piece, estimated ms of the rest's broadcast (pipelined when worth an extra piece)."""
-    a, b, c = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
-    lib().cbg_last_summa_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
-    return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value)
+    first piece, estimated ms of the rest's broadcast, and the ms an extra piece is taken
+    to cost (pipelined when the hidden broadcast is worth it)."""
+    a, b, c, d = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    lib().cbg_last_summa_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d))
+    return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value, piece_cost_ms=d.value)
 
 
 def merge_stats():

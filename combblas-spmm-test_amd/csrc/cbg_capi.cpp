@@ -479,11 +479,12 @@ int cbg_grid_agree(cbg_grid* g, int local_rc, int* agreed) {
   });
 }
 
-int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms) {
+int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms, double* piece_cost_ms) {
   const cbg::SummaInfo& i = cbg::summa_info();
   if (pieces) *pieces = i.pieces;
   if (bcast_ms_piece0) *bcast_ms_piece0 = i.bcast_ms_piece0;
   if (est_hidden_ms) *est_hidden_ms = i.est_hidden_ms;
+  if (piece_cost_ms) *piece_cost_ms = i.piece_cost_ms;
   return CBG_OK;
 }
 

@@ -158,7 +158,7 @@ MergeStats& merge_stats();
 // time of the first piece, and the transfer of the rest it estimated
 struct SummaInfo {
   int pieces = 0;
-  double bcast_ms_piece0 = 0, est_hidden_ms = 0;
+  double bcast_ms_piece0 = 0, est_hidden_ms = 0, piece_cost_ms = 0;
 };
 SummaInfo& summa_info();
 // A-side preparation (column maps of A) kept across the local multiplies of

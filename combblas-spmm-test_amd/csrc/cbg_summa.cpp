@@ -411,6 +411,15 @@ static double pipeline_min_ms() {
   static const char* e = getenv("CBG_PIPELINE_MIN_MS");
   return e ? atof(e) : 3.0;
 }
+// ... and on larger tiles a share of the rank's multiply (CBG_PIPELINE_COST_FRAC,
+// default 0.04: 1-7 % measured on the scale-22 2x1 rank tiles of 258 ms), taken
+// from this thread's previous adaptive PANEL call (the same product repeated)
+static thread_local double g_last_panel_ms = 0.0;
+static double pipeline_cost_ms() {
+  static const char* e = getenv("CBG_PIPELINE_COST_FRAC");
+  static const double frac = e ? atof(e) : 0.04;
+  return std::max(pipeline_min_ms(), frac * g_last_panel_ms);
+}
 
 static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                        const std::vector<int64_t>& cuts_in, cbg_phase_fn fn, void* user, cbg_tile* C,
@@ -492,7 +501,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   // Adaptive double buffering (PANEL with the default two pieces on a grid):
   // piece 0 (1/8 of B's columns) has been broadcast; its measured time, scaled
   // to the rest's bytes, is the transfer that pipelining would hide behind
-  // piece 0's multiply.  An extra piece costs about pipeline_min_ms() of
+  // piece 0's multiply.  An extra piece costs about pipeline_cost_ms() of
   // compute, so the ranks keep the two pieces only when the hidden transfer
   // is larger (agreed over the grid: every rank cuts its B tile alike);
   // otherwise the rest is broadcast at once and the pieces are rejoined into
@@ -513,7 +522,8 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     const double hidden = b0 > 0 ? ms0 * (double)b1 / (double)b0 : 0.0;
     info.bcast_ms_piece0 = ms0;
     info.est_hidden_ms = hidden;
-    const int want = hidden > pipeline_min_ms() ? 1 : 0;
+    info.piece_cost_ms = pipeline_cost_ms();
+    const int want = hidden > info.piece_cost_ms ? 1 : 0;
     const int dec = agree(g, local ? local : want);  // codes >= 3001 are failures
     if (dec > 1) {
       rc = dec;
@@ -553,6 +563,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   TileGuard Apanel;
   const cbg_tile* Ause = &A;
   int cb_rc = 0;
+  double panel_ms = 0.0;
   for (int p = 0; p < np && !rc; ++p) {
     local = std::max(local, step([&] { CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0)); }));
     if (p + 1 < np) {
@@ -581,7 +592,9 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
         Buse = &Bp.t;
       }
       TileGuard Cp;
-      local_spgemm(*Ause, *Buse, sr, Cp.t, cs, nullptr, arena.get());
+      LocalStats ls;
+      local_spgemm(*Ause, *Buse, sr, Cp.t, cs, &ls, arena.get());
+      panel_ms += ls.ms_symbolic + ls.ms_numeric;
       for (auto& t : Bc[p]) tile_free_device(t.t);
       tile_free_device(own[p].t);
       if (fn) {
@@ -595,6 +608,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     });
   }
   if (!rc) rc = agree(g, local);
+  if (!rc && adaptive) g_last_panel_ms = panel_ms;
   if (rc) {
     if (!g->broken) wait_comm(g);  // posted broadcasts complete before their buffers are released
     return rc;

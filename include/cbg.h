@@ -157,10 +157,12 @@ int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms
  * merged entries out, device ms */
 int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);
 /* last PANEL SUMMA call's double buffering: B-column pieces multiplied (1 = the
- * broadcast was not pipelined), measured broadcast ms of the first piece, and
- * the estimated broadcast ms of the rest that pipelining would hide (pipelined
- * when it exceeds CBG_PIPELINE_MIN_MS, default 3: the cost of an extra piece) */
-int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms);
+ * broadcast was not pipelined), measured broadcast ms of the first piece, the
+ * estimated broadcast ms of the rest that pipelining would hide, and the ms an
+ * extra piece is taken to cost: max(CBG_PIPELINE_MIN_MS (3), CBG_PIPELINE_COST_FRAC
+ * (0.04) x the previous such call's local multiply ms); pipelined when the
+ * hidden ms exceed the cost on some rank */
+int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms, double* piece_cost_ms);
 
 /* ---------------- 2D SUMMA over RCCL ---------------- */
 typedef struct cbg_grid cbg_grid;
