@@ -291,7 +291,7 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
 // The rows of A are cut into panels of P = 2^plog rows (P <= 2^18, so a
 // panel's bitmap is <= 32 KiB of LDS); A(:,k) restricted to panel r is a
 // contiguous run of A's column (rows are sorted), located once by
-// k_colmap_panels.  A big column j of B is then processed as R independent
+// k_colmap_panels_col.  A big column j of B is then processed as R independent
 // (j, r) sub-problems: C(panel r, j) = A(panel r, :) * B(:, j), whose sorted
 // outputs concatenate in panel order.  Each (j, r) is one workgroup in the
 // symbolic (bitmap -> counts, slab plan) and numeric (bitmap -> ranks ->
@@ -323,30 +323,36 @@ constexpr int BIG_BS = CBG_BIG_BS;
 constexpr int SPARSE_SLAB_MAX = 4096;   // products of a (column, panel) pair counted by hash -> hash slab
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 
-// cmapP[r * nA1 + k] = {first, end} positions of A(:,k)'s rows inside panel r.
-// A panel without rows of A(:,k) gets {q, q} with q the lower bound of the
-// panel's first row, so that {cmapP[r0].x, cmapP[r1].y} is A(:,k)'s run over
-// the panels r0..r1 (panel groups).  Columns absent from A stay {0, 0}.
-__global__ void k_colmap_panels(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
-                                const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
-                                int2* __restrict__ cmapP) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t i = t / FLOP_G;  // FLOP_G lanes per A column
+// Panel column maps of A: cmapP[r * (n+1) + k] = (first, end) of column k's
+// entries in row panel r.  A panel without rows of A(:,k) gets (q, q) with q
+// the lower bound of the panel's first row, so that (cmapP[r0].x,
+// cmapP[r1].y) is A(:,k)'s run over panels r0..r1 (panel groups); columns
+// absent from A stay (0, 0) (the caller's memset).  One
+// thread per nonempty A column walks its rows once (short columns) or
+// binary-searches each panel boundary (long ones) and writes its R entries,
+// so every store of a wave is one row of the map at consecutive columns
+// (coalesced; one thread per entry scattering over R rows was 3x slower).
+__global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
+                                    const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
+                                    int2* __restrict__ cmapP) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= nzcA) return;
-  const int64_t k = jcA[i], a = cpA[i], e = cpA[i + 1];
-  for (int64_t q = a + t % FLOP_G; q < e; q += FLOP_G) {
-    const int pnl = irA[q] >> plog;
-    const int prev = q == a ? -1 : irA[q - 1] >> plog;
-    const int next = q == e - 1 ? R : irA[q + 1] >> plog;
-    if (prev != pnl) {
-      for (int p = prev + 1; p < pnl; ++p) cmapP[p * nA1 + k] = make_int2((int)q, (int)q);
-      cmapP[pnl * nA1 + k].x = (int)q;
+  const int64_t k = jcA[i];
+  const int a = (int)cpA[i], e = (int)cpA[i + 1];
+  int pos = a;
+  for (int r = 0; r < R; ++r) {
+    const int lo = pos;
+    if (r == R - 1) {
+      pos = e;
+    } else {
+      const int bound = (r + 1) << plog;
+      if (e - pos <= 32) {
+        while (pos < e && irA[pos] < bound) ++pos;
+      } else {
+        pos = lower_bound_g(irA, pos, e, bound);
+      }
     }
-    if (next != pnl) {
-      cmapP[pnl * nA1 + k].y = (int)(q + 1);
-      if (q == e - 1)
-        for (int p = pnl + 1; p < R; ++p) cmapP[p * nA1 + k] = make_int2((int)e, (int)e);
-    }
+    cmapP[r * nA1 + k] = make_int2(lo, pos);
   }
 }
 
@@ -1998,8 +2004,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
         hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, cp.p);
       } else {
         CBG_HIP(hipMemsetAsync(cp.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
-        hipLaunchKernelGGL(k_colmap_panels, dim3(nblk(A.nzc * FLOP_G, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc,
-                           A.ir, bp.plog, bp.R, A.n + 1, cp.p);
+        hipLaunchKernelGGL(k_colmap_panels_col, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
+                           bp.plog, bp.R, A.n + 1, cp.p);
       }
       if (ap.active) ap.plog = bp.plog;
       bp.cmapP = cp.p;
