@@ -55,11 +55,19 @@ __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int3
 }
 
 // flops of every B column: FLOP_G lanes per column (B columns are short on
-// average; a whole wave per column would leave most lanes idle)
-constexpr int FLOP_G = 16;
+// average; a whole wave per column would leave most lanes idle).  A group
+// sums at most FLOP_HEAD entries of its column and queues a longer column
+// (R-MAT hubs: 10^4-10^5 entries, whose serial tail would set the kernel's
+// time) for k_flops_tail, where a whole block sums the rest.
+#ifndef CBG_FLOP_G  // scale 22, per phase: 8/512 0.52 ms, 16/512 0.76, 8/256 0.59, 4/512 0.57, 8/1024 0.54
+#define CBG_FLOP_G 8
+#define CBG_FLOP_HEAD 512
+#endif
+constexpr int FLOP_G = CBG_FLOP_G;
+constexpr int FLOP_HEAD = CBG_FLOP_HEAD;
 // flops[nzcB] accumulates the total (one atomic per block)
 __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                        const int2* __restrict__ cmap, int64_t* __restrict__ flops) {
+                        const int2* __restrict__ cmap, int64_t* __restrict__ flops, int* __restrict__ longq) {
   __shared__ unsigned long long bsum;
   if (threadIdx.x == 0) bsum = 0;
   __syncthreads();
@@ -67,8 +75,12 @@ __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int
   const int64_t w = t / FLOP_G;
   const int g = (int)(t % FLOP_G);
   long long s = 0;
-  if (w < nzcB)
-    for (int64_t p = cpB[w] + g; p < cpB[w + 1]; p += FLOP_G) s += cmap[irB[p]].y;
+  if (w < nzcB) {
+    const int64_t p0 = cpB[w], p1 = cpB[w + 1];
+    const int64_t pe = p1 - p0 > FLOP_HEAD ? p0 + FLOP_HEAD : p1;
+    for (int64_t p = p0 + g; p < pe; p += FLOP_G) s += cmap[irB[p]].y;
+    if (g == 0 && pe < p1) longq[1 + atomicAdd(&longq[0], 1)] = (int)w;
+  }
 #pragma unroll
   for (int d = FLOP_G / 2; d > 0; d >>= 1) s += __shfl_xor(s, d, FLOP_G);
   if (w < nzcB && g == 0) {
@@ -77,6 +89,29 @@ __global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int
   }
   __syncthreads();
   if (threadIdx.x == 0 && bsum) atomicAdd(reinterpret_cast<unsigned long long*>(flops + nzcB), bsum);
+}
+// the entries past FLOP_HEAD of the queued columns: a block per column
+// (grid-stride over the queue, whose length only the device knows)
+__global__ __launch_bounds__(256) void k_flops_tail(const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                    const int2* __restrict__ cmap, int64_t nzcB,
+                                                    int64_t* __restrict__ flops, const int* __restrict__ longq) {
+  __shared__ long long part[256 / WAVE];
+  const int nq = longq[0];
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int w = longq[1 + q];
+    long long s = 0;
+    for (int64_t p = cpB[w] + FLOP_HEAD + threadIdx.x; p < cpB[w + 1]; p += blockDim.x) s += cmap[irB[p]].y;
+    for (int d = WAVE / 2; d > 0; d >>= 1) s += __shfl_xor(s, d);
+    if (lane_id() == 0) part[threadIdx.x / WAVE] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      long long tot = 0;
+      for (int k = 0; k < 256 / WAVE; ++k) tot += part[k];
+      flops[w] += tot;  // this block owns column w's entry (k_flops wrote its head)
+      atomicAdd(reinterpret_cast<unsigned long long*>(flops + nzcB), (unsigned long long)tot);
+    }
+    __syncthreads();
+  }
 }
 
 // panel column map when A has a single row panel: {start, end} from cmap
@@ -1930,7 +1965,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
   CBG_HIP(hipMemsetAsync(flops.p + nz, 0, sizeof(int64_t), s));
-  hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p);
+  {
+    DBuf<int> longq(nz + 1);  // count | queued columns
+    CBG_HIP(hipMemsetAsync(longq.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p,
+                       longq.p);
+    hipLaunchKernelGGL(k_flops_tail, dim3((unsigned)std::min<int64_t>(nz, 1024)), dim3(256), 0, s, B.cp, B.ir, cmap.p,
+                       nz, flops.p, longq.p);
+    df.take(longq);
+  }
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
