@@ -341,6 +341,26 @@ __device__ __forceinline__ void bitonic_sort_kv(int* keys, double* vals, int tid
   }
 }
 
+// Ascending bitonic sort of one (key, val) per lane across the 64 lanes of a
+// wave, in registers (cross-lane swaps; no LDS, no barriers).  Used for the
+// 64-slot wave tables; for 2-8 slots per lane the LDS sort was as fast.
+__device__ __forceinline__ void wave_bitonic_sort_kv(int& key, double& val, int lane) {
+#pragma unroll
+  for (int k = 2; k <= WAVE; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int ok = __shfl_xor(key, j);
+      const double ov = __shfl_xor(val, j);
+      const bool up = (lane & k) == 0;     // this block of k lanes sorts ascending
+      const bool lower = (lane & j) == 0;  // lower lane of the pair keeps the min when ascending
+      if (lower == up ? ok < key : ok > key) {
+        key = ok;
+        val = ov;
+      }
+    }
+  }
+}
+
 // Emit the n occupied slots of an LDS hash table (keys[T], vals[T]; empty =
 // EMPTY_KEY) in ascending key order to out[obase ...] without a full sort:
 // keys are bucketed by (key - lo) >> bshift into NB buckets (counting sort),

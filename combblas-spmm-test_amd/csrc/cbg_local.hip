@@ -1007,9 +1007,19 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
         [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     wave_sync();
   }
-  bitonic_sort_kv<T, WAVE>(keys, vals, lane, WaveSync());
   const int64_t o = colptr[col];
   const int nout = (int)(colptr[col + 1] - o);
+  if constexpr (T == WAVE) {  // one slot per lane: sort in registers (-28 % kernel time)
+    int key = keys[lane];
+    double val = vals[lane];
+    wave_bitonic_sort_kv(key, val, lane);
+    if (lane < nout) {
+      st_stream(&out_ir[o + lane], key);
+      st_stream(&out_val[o + lane], val);
+    }
+    return;
+  }
+  bitonic_sort_kv<T, WAVE>(keys, vals, lane, WaveSync());
   for (int e = lane; e < nout; e += WAVE) {
     st_stream(&out_ir[o + e], keys[e]);
     st_stream(&out_val[o + e], vals[e]);
