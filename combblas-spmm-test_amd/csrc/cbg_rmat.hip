@@ -238,6 +238,9 @@ void rmat_tile(int scale, int ef, uint64_t userseed, int pr, int pc, int prow, i
   P.mper = nv / pr;
   P.nper = nv / pc;
   const int64_t M = nv * ef;
+  // hipcub's sort / run-length encode count items in int: 2^scale * ef < 2^31
+  // (scale 26 at ef 16; the configurations stop at 24)
+  if (M >= (int64_t)INT32_MAX) throw HipError("R-MAT generator: 2^scale * edgefactor must stay below 2^31", CBG_ERR_NOTSUPPORTED);
   const int64_t lm = (prow == pr - 1) ? nv - prow * P.mper : P.mper;
   const int64_t ln = (pcol == pc - 1) ? nv - pcol * P.nper : P.nper;
 
