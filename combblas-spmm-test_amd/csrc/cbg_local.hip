@@ -1349,6 +1349,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #ifndef CBG_EMIT_NB_DIV  // emit buckets of a hash slab: power of two <= T / DIV
 #define CBG_EMIT_NB_DIV 4
 #endif
+#ifndef CBG_HASH_MEMB_ALIAS  // emit member list in the idle staging arrays (3072-slot slabs: 3 blocks per CU, not 2)
+#define CBG_HASH_MEMB_ALIAS 0  // 1: +0.4 % at 22, -0.7 % at 18 (same box, 2 runs): within noise, off
+#endif
 template <int T_, int BS>
 struct SlabHashLds {
   static constexpr int T = T_;
@@ -1356,10 +1359,13 @@ struct SlabHashLds {
   static constexpr int NB = 1 << LOGNB;  // row buckets of the sorted emit (power of two <= T/4)
   static constexpr int MEMB = (T * CBG_HASH_LOAD_DEN + CBG_HASH_LOAD_NUM - 1) / CBG_HASH_LOAD_NUM;  // max nnz
   // vals[T] f64 | keys[T] | bv[BS] f64 | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
+  // bv|pref|st: idle during the emit, which reuses them for its in-bucket row
+  // offsets (u16, MOFF) and, where both fit, its member list
+  static constexpr int IDLE = BS * 8 + (BS + 4) * 4 + BS * 4;
+  static constexpr bool MOFF_FITS = MEMB * 2 <= IDLE;
+  static constexpr bool MEMB_ALIAS = CBG_HASH_MEMB_ALIAS && 2 * MEMB * 2 <= IDLE;
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
-                               (2 * NB + 4) * 4 + MEMB * 2;
-  // the emit's in-bucket row offsets (u16) reuse bv|pref|st, idle during the emit
-  static constexpr bool MOFF_FITS = MEMB * 2 <= BS * 8 + (BS + 4) * 4 + BS * 4;
+                               (2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2);
 };
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
@@ -1390,7 +1396,8 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   int* tmp = st + BS;
   int* boff = tmp + BS / WAVE + 4;
   int* cur = boff + NB + 4;
-  unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
+  unsigned short* members = L::MEMB_ALIAS ? reinterpret_cast<unsigned short*>(bv) + L::MEMB
+                                          : reinterpret_cast<unsigned short*>(cur + NB);
   const int tid = threadIdx.x;
   int i = blockIdx.x;
   if (i >= n) return;
