@@ -460,6 +460,55 @@ __device__ __forceinline__ void hash_emit_sorted(int* keys, double* vals, int lo
   }
 }
 
+// The same emit (MOFF) with each thread's slots kept in registers between the
+// counting and the scatter pass: the counting pass's returning atomic gives
+// every entry its index inside its bucket, so the scatter pass re-reads no key
+// and needs no second atomic.  The rank pass still walks the bucket-ordered
+// list (its output stores then land nearly in order: ranking each thread's
+// own slots instead scatters the stores over the slab, 2.3x slower).
+template <int T, int BS, int NB>
+__device__ __forceinline__ void hash_emit_reg(const int* keys, const double* vals, int lo, int bshift, int* boff,
+                                              int* cur, unsigned short* members, int* tmp, unsigned short* moff,
+                                              int32_t* __restrict__ out_ir, double* __restrict__ out_val,
+                                              int64_t obase) {
+  constexpr int E = (T + BS - 1) / BS;
+  const int tid = threadIdx.x;
+  const int omask = (1 << bshift) - 1;
+  for (int b = tid; b < NB; b += BS) cur[b] = 0;
+  __syncthreads();
+  int kk[E], ix[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int j = tid + e * BS;
+    kk[e] = (T % BS == 0 || j < T) ? keys[j] : EMPTY_KEY;
+    ix[e] = kk[e] != EMPTY_KEY ? atomicAdd(&cur[(kk[e] - lo) >> bshift], 1) : 0;
+  }
+  __syncthreads();
+  const int total = block_ordered_scan<BS>(
+      NB, [&](int b) { return cur[b]; }, [&](int b, int x) { boff[b] = x; }, tmp);
+  if (tid == 0) boff[NB] = total;
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (kk[e] != EMPTY_KEY) {
+      const int pos = boff[(kk[e] - lo) >> bshift] + ix[e];
+      members[pos] = (unsigned short)(tid + e * BS);
+      moff[pos] = (unsigned short)((kk[e] - lo) & omask);
+    }
+  __syncthreads();
+  for (int p = tid; p < total; p += BS) {
+    const int j = members[p];
+    const int k = keys[j];
+    const int b = (k - lo) >> bshift;
+    const int mo = (k - lo) & omask;
+    const int q0 = boff[b], q1 = boff[b + 1];
+    int r = q0;
+    for (int q = q0; q < q1; ++q) r += (int)moff[q] < mo;
+    st_emit(&out_ir[obase + r], k);
+    st_emit(&out_val[obase + r], vals[j]);
+  }
+}
+
 struct WaveSync {
   __device__ __forceinline__ void operator()() const { wave_sync(); }
 };

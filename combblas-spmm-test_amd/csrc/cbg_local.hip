@@ -1346,6 +1346,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
 #ifndef CBG_EMIT_MOFF  // emit ranks from cached in-bucket row offsets (1 LDS read per bucket member)
 #define CBG_EMIT_MOFF 1
 #endif
+#ifndef CBG_EMIT_REG  // hash_emit_reg: slots held in registers across the emit's passes
+#define CBG_EMIT_REG 1
+#endif
 #ifndef CBG_EMIT_NB_DIV  // emit buckets of a hash slab: power of two <= T / DIV
 #define CBG_EMIT_NB_DIV 4
 #endif
@@ -1489,7 +1492,10 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
     // in-bucket offsets fit u16 for panel-group slabs (span <= 2^(plog+4) rows,
     // bshift <= 15); whole-column bins (CMLEN) use them while bshift <= 16
     constexpr bool MOFF = L::MOFF_FITS && CBG_EMIT_MOFF;
-    if (MOFF && (!CMLEN || bshift <= 16))
+    if (MOFF && CBG_EMIT_REG && (!CMLEN || bshift <= 16))
+      hash_emit_reg<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp,
+                               reinterpret_cast<unsigned short*>(bv), out_ir, out_val, rec.obase);
+    else if (MOFF && (!CMLEN || bshift <= 16))
       hash_emit_sorted<T, BS, NB, MOFF>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val,
                                         rec.obase, reinterpret_cast<unsigned short*>(bv));
     else
