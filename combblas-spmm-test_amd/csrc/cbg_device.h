@@ -258,6 +258,15 @@ __device__ __forceinline__ void block_products(const int* pref, int total, S&& s
   block_products3<BS>(pref, total, seg, load, PreIdentity(), apply);
 }
 
+// Staged segments: st[sg] holds A's start minus the segment's first product
+// index (CBG_SEG_OFF=1), so a segment switch reads one LDS word less
+#ifndef CBG_SEG_OFF
+#define CBG_SEG_OFF 1
+#endif
+__device__ __forceinline__ int seg_stage(int s, int ex) { return CBG_SEG_OFF ? s - ex : s; }
+__device__ __forceinline__ int seg_off(const int* st, const int* pref, int sg) {
+  return CBG_SEG_OFF ? st[sg] : st[sg] - pref[sg];
+}
 // per-segment register cache: A offset (st[sg] - pref[sg]) and B value
 struct SegI {
   int off;

@@ -253,10 +253,10 @@ __global__ __launch_bounds__(256) void k_sym_wave(const int32_t* __restrict__ pe
     const int total = wave_last(incl);
     pref[lane + 1] = incl;
     if (lane == 0) pref[0] = 0;
-    st[lane] = s;
+    st[lane] = seg_stage(s, incl - len);
     wave_sync();
     wave_products(
-        pref, WAVE, 0, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        pref, WAVE, 0, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
         [&](const SegI& g, int u) { return irA[g.off + u]; },
         [&](int row) {
           count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row);
@@ -304,10 +304,10 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
-    st[tid] = s;
+    st[tid] = seg_stage(s, ex);
     __syncthreads();
     block_products<BS>(
-        pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
         [&](const SegI& g, int u) { return irA[g.off + u]; },
         [&](int row) {
           count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row);
@@ -508,7 +508,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
-    st[tid] = s;
+    st[tid] = seg_stage(s, ex);
     prod = total;
     hook(1);
     phase_mark(tmark, 8);
@@ -520,7 +520,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       __syncthreads();
       int count = 0;
       block_products<BS>(
-          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
           [&](const SegI& g, int u) { return irA[g.off + u]; },
           [&](int row) {
             count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
@@ -547,7 +547,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     __syncthreads();
     if (!(c_dbg & 1))
       block_products<BS>(
-          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
           [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
     __syncthreads();
@@ -567,12 +567,12 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
     prod += total;
-    st[tid] = s;
+    st[tid] = seg_stage(s, ex);
     hook(1);
     __syncthreads();
     if (!(c_dbg & 1))
       block_products<BS>(
-          pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+          pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
           [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
     __syncthreads();
@@ -690,7 +690,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   const int ex = block_excl_scan<BS>(len, L.tmp, &total);
   L.pref[tid] = ex;
   if (tid == BS - 1) L.pref[BS] = total;
-  L.st[tid] = s;
+  L.st[tid] = seg_stage(s, ex);
   hook(1);
   int T = 512;
   while (T * CBG_SYM_LOAD_DEN < CBG_SYM_LOAD_NUM * total) T <<= 1;
@@ -707,7 +707,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   const int* pref = L.pref;
   const int* st = L.st;
   block_products<BS>(
-      pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+      pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
       [&](const SegI& g, int u) { return irA[g.off + u]; },
       [&](int row) {
         count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
@@ -998,11 +998,11 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
     const int total = wave_last(incl);
     pref[lane + 1] = incl;
     if (lane == 0) pref[0] = 0;
-    st[lane] = s;
+    st[lane] = seg_stage(s, incl - len);
     bv[lane] = bval;
     wave_sync();
     wave_products(
-        pref, WAVE, 0, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        pref, WAVE, 0, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
         [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
         [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     wave_sync();
@@ -1072,11 +1072,11 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
-    st[tid] = s;
+    st[tid] = seg_stage(s, ex);
     bv[tid] = bval;
     __syncthreads();
     block_products<BS>(
-        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
         [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
         [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
     __syncthreads();
@@ -1122,13 +1122,13 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
   if (pass == 0) {
     block_products<BS>(
-        pref, total, [&](int sg) { return SegI{st[sg] - pref[sg]}; },
+        pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
         [&](const SegI& g, int u) { return irA[g.off + u] - lo; },
         [&](int r) { atomicOr(&bm[r >> 5], 1u << (r & 31)); });
   } else {
     // ranks of a group of products are looked up before any accumulates
     block_products3<BS>(
-        pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+        pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
         [&](const SegV& g, int u) { return a_rowval<SR>(irA, valA, g.off + u, g.b, lo); },
         [&](const RowVal& x) {
           const int w = x.row >> 5;
@@ -1228,7 +1228,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const int ex = block_excl_scan<BS>(len, tmp, &total);
       pref[tid] = ex;
       if (tid == BS - 1) pref[BS] = total;
-      st[tid] = tid < rec.nb ? p_ce.x : 0;
+      st[tid] = seg_stage(tid < rec.nb ? p_ce.x : 0, ex);
       bv[tid] = tid < rec.nb ? p_bv : 0.0;
     }
     __syncthreads();
@@ -1303,7 +1303,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           const int ex = block_excl_scan<BS>(len, tmp, &total);
           pref[tid] = ex;
           if (tid == BS - 1) pref[BS] = total;
-          st[tid] = s;
+          st[tid] = seg_stage(s, ex);
           bv[tid] = bval;
           __syncthreads();
           phase_mark(tmark, 1);
@@ -1472,13 +1472,13 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       const int ex = block_excl_scan<BS>(len, tmp, &total);
       pref[tid] = ex;
       if (tid == BS - 1) pref[BS] = total;
-      st[tid] = s;
+      st[tid] = seg_stage(s, ex);
       bv[tid] = bval;
       __syncthreads();
       phase_mark(tmark, 13);
       if (c == nch - 1 && has_next) fetch1(nrec);
       block_products<BS>(
-          pref, total, [&](int sg) { return SegV{st[sg] - pref[sg], bv[sg]}; },
+          pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
           [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
           [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
