@@ -1094,6 +1094,9 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 // into the LDS value slot of its rank.  No hashing, no sort, coalesced output.
 // Two launch classes by slab size so that small slabs run 2 workgroups per CU
 // (their phases overlap) while large ones get the full LDS for values.
+#ifndef CBG_ROWS_DIRECT  // bitmap slabs store C's rows from the bitmap words directly
+#define CBG_ROWS_DIRECT 1
+#endif
 template <int CAP, int BS>
 struct SlabLds {
   // vals[CAP] f64 | bv[BS] f64 | bm[SLAB_WORDS] | pref[BS+4] | st[BS] | tmp[BS/64+4] | (pad 16) wpre[SLAB_WORDS] u16
@@ -1318,7 +1321,20 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (has_next) fetch_stage2(nrec);
     // values: coalesced copy; rows: each word scatters its set bits to their
     // ranks in LDS (reusing the value array), then a coalesced copy
-    if (!(c_dbg & 8)) {
+    if (!(c_dbg & 8) && CBG_ROWS_DIRECT) {
+      // rows straight from the bitmap words to C (a wave's lanes hold
+      // consecutive words, so their ranks -- the store addresses -- are
+      // consecutive too): no LDS staging of the rows, no barriers
+      for (int w = tid; w < words; w += BS) {
+        unsigned x = bm[w];
+        int pos = wpre[w];
+        while (x) {
+          st_stream(&out_ir[obase + pos++], lo + w * 32 + __ffs(x) - 1);
+          x &= x - 1;
+        }
+      }
+      for (int j = tid; j < nout; j += BS) st_stream(&out_val[obase + j], vals[j]);
+    } else if (!(c_dbg & 8)) {
       for (int j = tid; j < nout; j += BS) st_stream(&out_val[obase + j], vals[j]);
       __syncthreads();
       int* rows = reinterpret_cast<int*>(vals);
