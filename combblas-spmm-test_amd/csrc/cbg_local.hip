@@ -1097,6 +1097,9 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 #ifndef CBG_ROWS_DIRECT  // bitmap slabs store C's rows from the bitmap words directly
 #define CBG_ROWS_DIRECT 1
 #endif
+#ifndef CBG_ROWS_DIRECT_NT  // ... as nontemporal stores: +66 GB of partial-line writes per scale-22 step
+#define CBG_ROWS_DIRECT_NT 0
+#endif
 template <int CAP, int BS>
 struct SlabLds {
   // vals[CAP] f64 | bv[BS] f64 | bm[SLAB_WORDS] | pref[BS+4] | st[BS] | tmp[BS/64+4] | (pad 16) wpre[SLAB_WORDS] u16
@@ -1329,7 +1332,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         unsigned x = bm[w];
         int pos = wpre[w];
         while (x) {
+#if CBG_ROWS_DIRECT_NT
           st_stream(&out_ir[obase + pos++], lo + w * 32 + __ffs(x) - 1);
+#else
+          out_ir[obase + pos++] = lo + w * 32 + __ffs(x) - 1;  // L2 merges the partial lines
+#endif
           x &= x - 1;
         }
       }
