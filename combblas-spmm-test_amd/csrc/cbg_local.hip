@@ -1094,6 +1094,9 @@ __global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ pe
 // into the LDS value slot of its rank.  No hashing, no sort, coalesced output.
 // Two launch classes by slab size so that small slabs run 2 workgroups per CU
 // (their phases overlap) while large ones get the full LDS for values.
+#ifndef CBG_VEC_INIT  // slab LDS initialisation with 16-byte stores
+#define CBG_VEC_INIT 1
+#endif
 #ifndef CBG_ROWS_DIRECT  // bitmap slabs store C's rows from the bitmap words directly
 #define CBG_ROWS_DIRECT 1
 #endif
@@ -1227,7 +1230,13 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const int j = k * BS + tid;
       if (j < words) bm[j] = have_bm ? pw[k] : 0u;
     }
-    for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
+    if (CBG_VEC_INIT) {  // 16-byte LDS stores (CAP is even, vals is 16-byte aligned)
+      const double id = Sem<SR>::identity();
+      double2* v2 = reinterpret_cast<double2*>(vals);
+      for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
+    } else {
+      for (int j = tid; j < nout; j += BS) vals[j] = Sem<SR>::identity();
+    }
     int total = 0;
     if (pre) {
       const int len = tid < rec.nb ? p_ce.y - p_ce.x : 0;
@@ -1463,9 +1472,17 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
     if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
     const bool pre = staged(rec);
     unsigned long long tmark = wall_clock64();
-    for (int j = tid; j < T; j += BS) {
-      keys[j] = EMPTY_KEY;
-      vals[j] = Sem<SR>::identity();
+    if (CBG_VEC_INIT) {  // 16-byte LDS stores (T is a multiple of 256; vals and keys are 16-byte aligned)
+      const double id = Sem<SR>::identity();
+      double2* v2 = reinterpret_cast<double2*>(vals);
+      int4* k4 = reinterpret_cast<int4*>(keys);
+      for (int j = tid; j < T / 2; j += BS) v2[j] = make_double2(id, id);
+      for (int j = tid; j < T / 4; j += BS) k4[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
+    } else {
+      for (int j = tid; j < T; j += BS) {
+        keys[j] = EMPTY_KEY;
+        vals[j] = Sem<SR>::identity();
+      }
     }
     __syncthreads();
     phase_mark(tmark, 7);
