@@ -7,10 +7,11 @@
 One step = one complete Mult_AnXBn_DoubleBuff (reference ParFriends.h:798-997)
 of Graph500 R-MAT A (SEED 0xDECAFBAD, ef 16, duplicates summed, loops removed)
 by a deep copy of A, inputs resident in HBM in the 2D block layout.  Every N
-runs the metric's scale 22.  N=1: C (297 GB) exceeds one GPU's HBM, so the
-multiply runs as MemEfficientSpGEMM with 3 B-column phases (ParFriends.h:449),
-each phase's C materialized in HBM and released; N>1: C left resident per
-tile.  N>1 is launched by torch.distributed.run, one rank per GPU, RCCL
+runs the metric's scale 22 as MemEfficientSpGEMM (ParFriends.h:449) whose
+phase count the library picks from device memory inside every step (N=1: C is
+297 GB, more than one GPU's HBM: 3 B-column phases, each phase's C
+materialized in HBM and handed to the consumer; a C tile that fits runs as one
+phase, the adaptive double-buffered DoubleBuff).  N>1 is launched by torch.distributed.run, one rank per GPU, RCCL
 row/column communicators (grid 2x1, 2x2, 4x2 for 2/4/8).  --scale 18 gives
 configs[1] (C resident on one GPU).
 
@@ -43,7 +44,7 @@ def load_cbg():
 # (broadcast piece by piece behind the multiply); measured per rank tile on one
 # GPU: 2x1 7 % and 4x2 2-13 % faster than 1x2 / 2x4.  --grid RxC overrides.
 GRIDS = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2), 9: (3, 3), 16: (4, 4)}
-ROUND = "r02"
+ROUND = "r03"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -58,8 +59,8 @@ def parse():
     p.add_argument("--algo", choices=["doublebuff", "synch"], default="doublebuff")
     p.add_argument("--exec", dest="exec_mode", choices=["panel", "staged"], default="panel")
     p.add_argument("--phases", type=int, default=None,
-                   help="MemEfficientSpGEMM phases (B column pieces); >1 streams C per phase "
-                        "(for C larger than HBM, e.g. scale 22 on one GPU)")
+                   help="MemEfficientSpGEMM phases (B column pieces): 0 (default) picks them from device "
+                        "memory per call and streams C per phase; 1 keeps C resident; P > 1 forces P")
     p.add_argument("--phase-consumer", choices=["none", "digest"], default="none",
                    help="what the phase callback does with each phase's device C tile")
     p.add_argument("--grid", default=None, help="RxC process grid (default: GRIDS[N])")
@@ -100,7 +101,7 @@ def pmc_traffic(scale, ef, phases):
     committed PMC passes (profiles/<round>_traffic_s<scale>.json, made by
     tools/profile_round.sh + tools/traffic.py: FETCH_SIZE calibrated on k_digest,
     + WRITE_SIZE), this round's file first, or None."""
-    for rnd in (ROUND, "r01"):
+    for rnd in (ROUND, "r02", "r01"):
         path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (rnd, scale))
         if not os.path.exists(path):
             continue
@@ -160,7 +161,7 @@ def cpu_baseline_reference(scale, ef, threads, algos=("synch",)):
 def cpu_baseline_s22():
     """The one-off reference run at the metric's own scale (profiles/<round>_cpu_reference_s22.json,
     tools/cpu_reference_s22.sh on the GPU box: Mult_AnXBn_Synch per B-column phase)."""
-    for rnd in (ROUND, "r01"):
+    for rnd in (ROUND, "r02", "r01"):
         path = os.path.join(REPO, "profiles", "%s_cpu_reference_s22.json" % rnd)
         if os.path.exists(path):
             with open(path) as f:
@@ -201,21 +202,15 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     N = max(world, 1)
     scale = a.scale if a.scale is not None else 22
+    # phases: 0 (default) = MemEfficientSpGEMM picks them from device memory on
+    # every call, inside the timed step (ParFriends.h:482-535; see
+    # cbg_summa_spgemm_memeff): scale 22 on one GPU (C = 297 GB) streams C per
+    # B-column phase, a C tile that fits runs as one phase (the adaptive
+    # double-buffered DoubleBuff).  --phases 1 keeps C resident (Mult_AnXBn_*),
+    # --phases P > 1 forces P phases.
     if a.phases is None:
-        # C streamed per B-column phase where a rank's C tile does not fit its
-        # HBM: scale 22 on one GPU (297 GB: 3 phases; 2 run out of HBM), scale
-        # 24 on 8 (about 275 GB per rank); otherwise phases of
-        # at most ~80 GB of C (nnz(C) per scale from the reference's symbolic
-        # totals, tests/golden/golden.json: s22 2.48e10, s24 1.83e11; s22 ef8
-        # 9.08e9 = 109 GB, resident on one GPU as SURVEY 8(d) asks)
-        nnz_est = {(22, 16): 2.48e10, (24, 16): 1.83e11, (22, 8): 9.08e9}.get(
-            (scale, a.ef), 2.48e10 * 7.4 ** ((scale - 22) / 2.0) * (a.ef / 16.0) ** 1.45)
-        per_rank = 12.0 * nnz_est / N
-        if N == 1 and scale == 22 and a.ef == 16:
-            a.phases = 3  # 99 GB of C per phase; 3 vs 4 phases: 506-508 vs 509-511 ms (same box)
-        else:
-            a.phases = 1 if per_rank < 150e9 else int(-(-per_rank // 80e9))
-    stream_c = a.phases > 1
+        a.phases = 0
+    stream_c = a.phases != 1
     rehearsal = N > 1 and os.environ.get("CBG_RANK_HOSTIDS") == "1"
     if rehearsal:
         # several ranks on ONE GPU (a development box): one NCCL_HOSTID per rank
@@ -286,9 +281,11 @@ def main():
                 t.digest(0, off)
 
         cbg.MemEfficientSpGEMM(A, B, a.phases, algo=algo, exec_mode=exec_mode, on_phase=consume)
+        plans.append(cbg.phase_plan())
         return seen[0], None
 
     C = None
+    plans = []
     for _ in range(a.warmup):
         _, C = step()
         if C is not None:
@@ -332,8 +329,9 @@ def main():
     achieved = bytes_alg / (ms_avg * 1e-3) / 1e9
     achieved = grid.allreduce_max(achieved) if N > 1 else achieved
 
+    phases_run = plans[-1]["phases"] if plans else 1
     if rank == 0:
-        traffic, traffic_src = pmc_traffic(scale, a.ef, a.phases) if N == 1 else (None, None)
+        traffic, traffic_src = pmc_traffic(scale, a.ef, phases_run) if N == 1 else (None, None)
         peaks += [cbg.hbm_copy_bandwidth(4 << 30, 10) for _ in range(2)]
         peak_measured = max(peaks)
         out = {
@@ -359,7 +357,15 @@ def main():
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
                 "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport,
-                "phases": a.phases,
+                "phases": phases_run,
+                "phase_plan": ({"automatic": plans[-1]["automatic"], "phases_per_step": [p_["phases"] for p_ in plans[-a.steps:]],
+                                "flops_rank0": plans[-1]["flops"], "nnz_est_rank0": plans[-1]["nnz_est"],
+                                "c_budget_gb_rank0": round(plans[-1]["c_budget_bytes"] / 1e9, 1),
+                                "oom_splits": plans[-1]["oom_splits"],
+                                "rule": "MemEfficientSpGEMM(phases=0): flops of the rank's product from tile count "
+                                        "vectors x the compression of an exact symbolic of every 64th B column, "
+                                        "12 B per entry against half of the free HBM, inside each timed step"}
+                               if plans else None),
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
                                      "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],
                                      "est_hidden_ms": [round(p_["est_hidden_ms"], 3) for p_ in pipe],

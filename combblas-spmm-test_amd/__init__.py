@@ -38,7 +38,7 @@ DOUBLEBUFF, SYNCH = 0, 1
 EXEC_PANEL, EXEC_STAGED = 0, 1
 
 GRIDMISMATCH, DIMMISMATCH, NOTSQUARE, MATRIXALIAS, INVALIDPARAMS = 3001, 3002, 3003, 3005, 3007
-NOTSUPPORTED = 3103
+HIPERROR, RCCLERROR, OOM, NOTSUPPORTED = 3100, 3101, 3102, 3103
 
 
 class CbgError(RuntimeError):
@@ -71,7 +71,8 @@ EXPORTS = [
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
     "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
-    "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info",
+    "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info", "cbg_summa_spgemm_memeff",
+    "cbg_last_phase_plan",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -127,6 +128,9 @@ def lib():
         "cbg_summa_spgemm": ([vp, T, T, i64, i64, i32, i32, i32, T], i32),
         "cbg_tile_equal": ([T, T, ctypes.c_double, ctypes.POINTER(i32)], i32),
         "cbg_summa_spgemm_phased": ([vp, T, T, i64, i64, i32, i32, i32, i32, PHASE_FN, vp, T], i32),
+        "cbg_summa_spgemm_memeff": ([vp, T, T, i64, i64, i32, i32, i32, i32, i64, PHASE_FN, vp, T], i32),
+        "cbg_last_phase_plan": ([ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)], i32),
         "cbg_tile_transpose": ([T, T], i32),
         "cbg_tile_dim_apply": ([T, i32, ctypes.POINTER(ctypes.c_double), i32], i32),
         "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
@@ -383,6 +387,17 @@ def summa_info():
     a, b, c, d = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     lib().cbg_last_summa_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d))
     return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value, piece_cost_ms=d.value)
+
+
+def phase_plan():
+    """the last MemEfficientSpGEMM's phases: count, whether chosen from memory, this
+    rank's product flops and nnz(C) estimate, the C bytes a phase was allowed, and
+    phases split in column halves after an out-of-memory."""
+    a, b, c, d, e, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int()
+    lib().cbg_last_phase_plan(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d), ctypes.byref(e),
+                              ctypes.byref(f))
+    return dict(phases=a.value, automatic=bool(b.value), flops=c.value, nnz_est=d.value, c_budget_bytes=e.value,
+                oom_splits=f.value)
 
 
 def merge_stats():
@@ -964,9 +979,13 @@ def Mult_AnXBn_Synch(A, B, sr=PlusTimesSRing, exec_mode=EXEC_PANEL):
 
 
 def MemEfficientSpGEMM(A, B, phases, sr=PlusTimesSRing, algo=DOUBLEBUFF, exec_mode=EXEC_PANEL, on_phase=None,
-                       hardThreshold=0.0, selectNum=0, recoverNum=0, recoverPct=0.0):
+                       hardThreshold=0.0, selectNum=0, recoverNum=0, recoverPct=0.0, perProcessMemory=0):
     """ParFriends.h:449-730 with `phases` column pieces of B; the MCL pruning
     arguments must stay at their no-pruning values (pruning is not on this path).
+
+    perProcessMemory > 0 (GB, ParFriends.h:482-535) or phases <= 0 (this
+    library's extension: the device's free memory) picks the phase count from
+    memory (see cbg_summa_spgemm_memeff; phase_plan() reports it).
 
     on_phase=None: C is the column concatenation of the phase products
     (ColConcatenate).  on_phase=fn: fn(phase, col_offset, Tile) is called with
@@ -989,8 +1008,9 @@ def MemEfficientSpGEMM(A, B, phases, sr=PlusTimesSRing, algo=DOUBLEBUFF, exec_mo
 
     fn = PHASE_FN(_cb) if on_phase is not None else PHASE_FN()
     C = Tile() if on_phase is None else None
-    rc = lib().cbg_summa_spgemm_phased(A.grid.h, ctypes.byref(A.tile.c), ctypes.byref(B.tile.c), A.gn, B.gm, _sr(sr),
-                                       algo, exec_mode, phases, fn, None, ctypes.byref(C.c) if C else None)
+    rc = lib().cbg_summa_spgemm_memeff(A.grid.h, ctypes.byref(A.tile.c), ctypes.byref(B.tile.c), A.gn, B.gm, _sr(sr),
+                                       algo, exec_mode, phases, int(perProcessMemory), fn, None,
+                                       ctypes.byref(C.c) if C else None)
     if errors:
         raise errors[0]
     _check(rc)

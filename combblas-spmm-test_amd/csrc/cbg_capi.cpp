@@ -21,7 +21,7 @@ void barrier(cbg_grid* g);
 int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr, int algo,
                  int exec, cbg_tile& C);
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
-                        int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C);
+                        int algo, int exec, int phases, int64_t mem_gb, cbg_phase_fn fn, void* user, cbg_tile* C);
 int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out);
 int agree(cbg_grid* g, int rc);
 std::string& step_error();
@@ -269,14 +269,18 @@ int cbg_restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, in
   });
 }
 
+static const char* summa_msg(int rc);
+
 int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out) {
   if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
   if (int rc = check_tile(local, true, "tile")) return rc;
   if (!out) return fail(CBG_ERR_INVALIDPARAMS, "out is NULL");
   return guard([&]() -> int {
     CBG_HIP(hipDeviceSynchronize());
+    cbg::step_error().clear();
     int rc = cbg::grid_transpose(g, *local, *out);
-    if (rc) return fail(rc, "SpParMat::Transpose needs a square grid");
+    if (rc == CBG_ERR_NOTSQUARE) return fail(rc, "SpParMat::Transpose needs a square grid");
+    if (rc) return fail(rc, cbg::step_error().empty() ? summa_msg(rc) : "this rank: " + cbg::step_error());
     return CBG_OK;
   });
 }
@@ -288,8 +292,11 @@ int cbg_grid_block_extract(cbg_grid* g, const cbg_tile* local, int64_t gm, int64
   if (!out) return fail(CBG_ERR_INVALIDPARAMS, "out is NULL");
   return guard([&]() -> int {
     CBG_HIP(hipDeviceSynchronize());
+    cbg::step_error().clear();
     int rc = cbg::grid_block_extract(g, *local, gm, gn, dim, lo, hi, *out);
-    if (rc) return fail(rc, "block range outside the matrix or bad dim");
+    if (rc == CBG_ERR_INVALIDPARAMS && cbg::step_error().empty())
+      return fail(rc, "block range outside the matrix or bad dim");
+    if (rc) return fail(rc, cbg::step_error().empty() ? summa_msg(rc) : "this rank: " + cbg::step_error());
     return CBG_OK;
   });
 }
@@ -320,13 +327,15 @@ int cbg_local_spgemm(const cbg_tile* A, const cbg_tile* B, int sr, cbg_tile* C, 
 }
 
 int cbg_local_symbolic(const cbg_tile* A, const cbg_tile* B, int64_t* flops, int64_t* nnz, void* stream) {
-  // the symbolic totals are a by-product of a full multiply's statistics
-  cbg_tile C{};
-  int rc = cbg_local_spgemm(A, B, CBG_PLUS_TIMES, &C, stream);
-  if (rc) return rc;
-  if (flops) *flops = cbg::thread_stats().flops;
-  if (nnz) *nnz = cbg::thread_stats().nnz;
-  return cbg_tile_free(&C);
+  if (int rc = check_tile(A, true, "A")) return rc;
+  if (int rc = check_tile(B, true, "B")) return rc;
+  if (A->n != B->m) return fail(CBG_ERR_DIMMISMATCH, "A.ncol != B.nrow");
+  if (A->nnz >= INT32_MAX || B->nnz >= INT32_MAX) return fail(CBG_ERR_NOTSUPPORTED, "A/B tiles need nnz < 2^31");
+  // the multiply's flops and symbolic kernels only: no C is formed
+  return guard([&] {
+    cbg::local_symbolic(*A, *B, as_stream(stream), flops, nnz);
+    return CBG_OK;
+  });
 }
 
 int cbg_merge(const cbg_tile* parts, int nparts, int sr, cbg_tile* C, void* stream) {
@@ -452,8 +461,9 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t 
   });
 }
 
-int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow,
-                            int sr, int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+int cbg_summa_spgemm_memeff(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow,
+                            int sr, int algo, int exec, int phases, int64_t per_process_memory_gb, cbg_phase_fn fn,
+                            void* user, cbg_tile* C) {
   if (!g) return fail(CBG_ERR_INVALIDPARAMS, "grid is NULL");
   // A and B may alias: B is copied (ParFriends.h:547-549)
   int arg = summa_args(A, B, sr, algo, exec);
@@ -465,10 +475,28 @@ int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, i
     if (arg) return fail(cbg::agree(g, arg), why);  // before any device call: peers must not block
     CBG_HIP(hipDeviceSynchronize());
     cbg::step_error().clear();
-    int rc = cbg::summa_spgemm_phased(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, phases, fn, user, C);
+    int rc = cbg::summa_spgemm_phased(g, *A, *B, A_gncol, B_gnrow, sr, algo, exec, phases, per_process_memory_gb, fn,
+                                      user, C);
     if (rc) return fail(rc, cbg::step_error().empty() ? summa_msg(rc) : "this rank: " + cbg::step_error());
     return CBG_OK;
   });
+}
+
+int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, int64_t A_gncol, int64_t B_gnrow,
+                            int sr, int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+  return cbg_summa_spgemm_memeff(g, A, B, A_gncol, B_gnrow, sr, algo, exec, phases, 0, fn, user, C);
+}
+
+int cbg_last_phase_plan(int* phases, int* automatic, int64_t* flops, int64_t* nnz_est, double* c_budget_bytes,
+                        int* oom_splits) {
+  const cbg::PhasePlan& p = cbg::phase_plan();
+  if (phases) *phases = p.phases;
+  if (automatic) *automatic = p.automatic;
+  if (flops) *flops = p.flops;
+  if (nnz_est) *nnz_est = p.nnz_est;
+  if (c_budget_bytes) *c_budget_bytes = p.c_budget_bytes;
+  if (oom_splits) *oom_splits = cbg::summa_info().oom_splits;
+  return CBG_OK;
 }
 
 int cbg_grid_agree(cbg_grid* g, int local_rc, int* agreed) {

@@ -159,7 +159,17 @@ MergeStats& merge_stats();
 struct SummaInfo {
   int pieces = 0;
   double bcast_ms_piece0 = 0, est_hidden_ms = 0, piece_cost_ms = 0;
+  int oom_splits = 0;  // phases computed as column halves after an out-of-memory
 };
+// the last MemEfficientSpGEMM call's phase plan: phases run, and when they
+// were chosen from memory, this rank's product flops, estimated nnz(C) and
+// the C bytes a phase may take
+struct PhasePlan {
+  int phases = 0, automatic = 0;
+  int64_t flops = 0, nnz_est = 0;
+  double c_budget_bytes = 0;
+};
+PhasePlan& phase_plan();
 SummaInfo& summa_info();
 // A-side preparation (column maps of A) kept across the local multiplies of
 // one MemEfficientSpGEMM call, whose phases all multiply the same A: between
@@ -219,6 +229,16 @@ void tile_concat_cols(const std::vector<cbg_tile>& parts, const std::vector<int6
 void tile_concat_rows(const std::vector<cbg_tile>& parts, const std::vector<int64_t>& row_off, int64_t m,
                       int64_t n, cbg_tile& out, hipStream_t s);
 bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s);
+// phase planning: dim 0 = nonzeros per column (length n), 1 = per row (length m),
+// into the device array d zero-padded to `padded` entries (stream synchronized)
+void tile_counts_device(const cbg_tile& t, int dim, int32_t* d, int64_t padded, hipStream_t s);
+// sum_k a[k] * b[k] over k < K with a, b stored as blocks (see cbg_tile.hip)
+int64_t blocked_dot_device(const int32_t* a, int64_t astride, const std::vector<int64_t>& aoff, const int32_t* b,
+                           int64_t bstride, const std::vector<int64_t>& boff, int64_t K, hipStream_t s);
+// every stride-th nonempty column of T (same shape and column ids)
+void tile_sample_cols(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s);
+// estimateFLOP + estimateNNZ_Hash totals of A*B without the numeric phase
+void local_symbolic(const cbg_tile& A, const cbg_tile& B, hipStream_t s, int64_t* flops, int64_t* nnz);
 
 // Galerkin path operations (cbg_ops.hip)
 void tile_transpose(const cbg_tile& T, cbg_tile& out, hipStream_t s);

@@ -1571,7 +1571,7 @@ __global__ void k_col_scatter(int64_t n, const int32_t* __restrict__ cnt, const 
 // host orchestration
 // ----------------------------------------------------------------------------
 void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st,
-                       OutSink* sink);
+                       OutSink* sink, bool sym_only = false);
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 static int device_cus() {
@@ -1958,8 +1958,20 @@ void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& 
   if (st) *st = mine;
 }
 
+// estimateFLOP + estimateNNZ_Hash (mtSpGEMM.h:1056-1134, 805-933) alone: the
+// multiply's flops, binning and symbolic kernels (no bitmaps kept), totals read
+// back, no C
+void local_symbolic(const cbg_tile& A, const cbg_tile& B, hipStream_t s, int64_t* flops, int64_t* nnz) {
+  cbg_tile C{};
+  LocalStats st;
+  local_spgemm_impl(A, B, CBG_PLUS_TIMES, C, s, &st, nullptr, true);
+  tile_free_device(C);
+  if (flops) *flops = st.flops;
+  if (nnz) *nnz = st.nnz;
+}
+
 void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s, LocalStats* st,
-                       OutSink* sink) {
+                       OutSink* sink, bool sym_only) {
   C = cbg_tile{};
   C.m = A.m;
   C.n = B.n;
@@ -2091,7 +2103,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<float>& valf = ap.active ? ap.valf : valf_own;
   int af = ap.active ? ap.af : -1, af_inexact = 0;
   DBuf<int> af_flag;
-  if (nbig > 0 && af < 0 && af32_enabled()) {
+  if (nbig > 0 && af < 0 && af32_enabled() && !sym_only) {
     valf.reset(A.nnz);
     af_flag.reset(1);
     CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
@@ -2123,7 +2135,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     // (saves the numeric marking pass); otherwise numeric rebuilds them
     // slots are handed out in launch order by the bitmap-mode pairs
     const int64_t slot_bytes = (int64_t)4 << (bp.plog - 5);
-    const int64_t nslots = std::min<int64_t>(nbr, (int64_t)(bitmap_budget_bytes() / slot_bytes));
+    const int64_t nslots = sym_only ? 0 : std::min<int64_t>(nbr, (int64_t)(bitmap_budget_bytes() / slot_bytes));
     DBuf<int> gbm_next;
     if (nslots > 0) {
       bp.gbm.reset((size_t)nslots << (bp.plog - 5));
@@ -2187,12 +2199,35 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   CBG_HIP(hipMemcpyAsync(&flops_total, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));  // host sync 2 of 4
+  if (sym_only) {
+    df.synced = true;
+    if (st) {
+      float a = 0;
+      CBG_HIP(hipEventElapsedTime(&a, ev0, ev1));
+      *st = LocalStats{};
+      st->ms_symbolic = a;
+      st->nnz = nnzc;
+      st->n_big = nbig;
+      st->flops = flops_total;
+    }
+    return;
+  }
   if (af_flag.p) {
     af = af_inexact ? 0 : 1;
     if (ap.active) ap.af = af;
     if (!af) valf.release();
   }
   if (af == 1) bp.valAf = valf.p;
+  {
+    // test hook (CBG_FAULT_C_BYTES, read per call): C larger than this fails as
+    // an out-of-memory would, after the symbolic pass -- the phase splitting of
+    // MemEfficientSpGEMM (cbg_summa.cpp multiply_to_fn) is tested with it
+    const char* e = getenv("CBG_FAULT_C_BYTES");
+    if (e && 12.0 * (double)nnzc > atof(e)) {
+      df.synced = true;
+      throw HipError("C of " + std::to_string(nnzc) + " entries exceeds CBG_FAULT_C_BYTES", CBG_ERR_OOM);
+    }
+  }
   C.nzc = nzcC;
   C.cp = static_cast<int64_t*>(pool().alloc(sizeof(int64_t) * (nzcC + 1)));
   C.jc = static_cast<int32_t*>(pool().alloc(sizeof(int32_t) * std::max<int64_t>(nzcC, 1)));

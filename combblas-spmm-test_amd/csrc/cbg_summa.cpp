@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -72,6 +73,7 @@ struct cbg_grid {
   hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timing of the first piece's broadcast
   bool broken = false;  // communicators aborted: every later collective fails
   int64_t calls = 0;    // SUMMA calls made on this grid (fault-injection index)
+  int64_t redist_calls = 0;  // Transpose / BlockSplit calls (CBG_FAULT_INJECT_REDIST index)
   bool fault_armed = false;
 };
 
@@ -241,6 +243,43 @@ void allgather_i64(cbg_grid* g, int which, const int64_t* in, int64_t* out, int 
   wait_comm(g);
 }
 
+// allgather of `bytes` bytes per rank (host buffers)
+static void allgather_bytes(cbg_grid* g, int which, const void* in, void* out, size_t bytes) {
+  check_usable(g);
+  const int P = comm_size(g, which);
+  if (bytes == 0) return;
+  if (g->host_mode) {
+    if (P == 1) {
+      std::memcpy(out, in, bytes);
+      return;
+    }
+    host_check(g, g->hc.allgather(g->hc.user, which, in, out, bytes), "allgather");
+    return;
+  }
+  DBuf<char> d((size_t)(P + 1) * bytes);
+  CBG_HIP(hipMemcpyAsync(d.p + P * bytes, in, bytes, hipMemcpyHostToDevice, g->comm));
+  CBG_NCCL(ncclAllGather(d.p + P * bytes, d.p, bytes, ncclInt8, pick(g, which), g->comm));
+  CBG_HIP(hipMemcpyAsync(out, d.p, (size_t)P * bytes, hipMemcpyDeviceToHost, g->comm));
+  wait_comm(g);
+}
+
+// allgather of `bytes` bytes per rank of DEVICE buffers (stream-ordered on the
+// comm stream and waited for); the host transport stages through host memory
+static void allgather_device(cbg_grid* g, int which, const void* in, void* out, size_t bytes) {
+  check_usable(g);
+  if (bytes == 0) return;
+  const int P = comm_size(g, which);
+  if (g->host_mode) {
+    std::vector<char> h(bytes), all((size_t)P * bytes);
+    CBG_HIP(hipMemcpy(h.data(), in, bytes, hipMemcpyDeviceToHost));
+    allgather_bytes(g, which, h.data(), all.data(), bytes);
+    CBG_HIP(hipMemcpy(out, all.data(), all.size(), hipMemcpyHostToDevice));
+    return;
+  }
+  CBG_NCCL(ncclAllGather(in, out, bytes, ncclInt8, pick(g, which), g->comm));
+  wait_comm(g);
+}
+
 void allreduce_f64(cbg_grid* g, double* v, bool max) {
   check_usable(g);
   if (g->host_mode) {
@@ -282,6 +321,22 @@ int agree(cbg_grid* g, int rc) {
   for (auto x : all) w = std::max(w, x);
   return (int)w;
 }
+// agree() that also reduces one value over the world: *vmin / *vmax receive
+// its minimum / maximum (one allgather, the same point of the protocol)
+static int agree_val(cbg_grid* g, int rc, int64_t val, int64_t* vmin, int64_t* vmax) {
+  int64_t v[2] = {rc, val};
+  std::vector<int64_t> all((size_t)2 * g->nranks);
+  allgather_i64(g, COMM_WORLD, v, all.data(), 2);
+  int64_t w = 0, lo = val, hi = val;
+  for (int r = 0; r < g->nranks; ++r) {
+    w = std::max(w, all[2 * r]);
+    lo = std::min(lo, all[2 * r + 1]);
+    hi = std::max(hi, all[2 * r + 1]);
+  }
+  if (vmin) *vmin = lo;
+  if (vmax) *vmax = hi;
+  return (int)w;
+}
 
 // Test hook (CBG_FAULT_INJECT="rank:k1,k2,..."): in the listed SUMMA calls
 // that rank `rank` makes on a grid (counted from 0 over the grid's life), the
@@ -305,6 +360,25 @@ static void maybe_inject_fault(cbg_grid* g) {
   if (!g->fault_armed) return;
   g->fault_armed = false;
   throw HipError("injected fault (CBG_FAULT_INJECT) in SUMMA call " + std::to_string(g->calls - 1), CBG_ERR_OOM);
+}
+// the same for the redistributions (Transpose, BlockSplit):
+// CBG_FAULT_INJECT_REDIST="rank:k1,k2,..." counts their calls on a grid, and
+// the listed calls of that rank fail their receive-buffer allocation as an
+// out-of-memory would
+static bool redist_fault(cbg_grid* g) {
+  static const char* e = getenv("CBG_FAULT_INJECT_REDIST");
+  const int64_t k = g->redist_calls++;
+  if (!e) return false;
+  const char* c = strchr(e, ':');
+  if (!c || atoi(e) != g->rank) return false;
+  for (const char* q = c + 1; *q;) {
+    char* end = nullptr;
+    const long long at = strtoll(q, &end, 10);
+    if (end == q) break;
+    if (at == k) return true;
+    q = *end == ',' ? end + 1 : end;
+  }
+  return false;
 }
 
 // code of a failure inside a collective step (the step's exception is not
@@ -419,6 +493,37 @@ static double pipeline_cost_ms() {
   static const char* e = getenv("CBG_PIPELINE_COST_FRAC");
   static const double frac = e ? atof(e) : 0.04;
   return std::max(pipeline_min_ms(), frac * g_last_panel_ms);
+}
+
+// One phase's local multiply handed to fn (MemEfficientSpGEMM with a phase
+// consumer).  A phase whose C does not fit the device -- the multiply learns
+// nnz(C) from its symbolic pass and its allocation fails with CBG_ERR_OOM
+// before any output is written -- is computed as two column halves of its B
+// piece, each handed to fn with the same phase index and its own column
+// offset, so an underestimated phase count costs a repeated symbolic pass, not
+// the job.  The split is local: the piece's B columns are already on this rank.
+static void multiply_to_fn(const cbg_tile& A, const cbg_tile& B, int sr, hipStream_t cs, int p, int64_t off,
+                           cbg_phase_fn fn, void* user, int& cb_rc, double& ms, int depth) {
+  TileGuard Cp;
+  LocalStats ls;
+  try {
+    local_spgemm(A, B, sr, Cp.t, cs, &ls, nullptr);
+  } catch (const HipError& e) {
+    if (e.code != CBG_ERR_OOM || B.n < 2 || depth >= 12) throw;
+    pool().trim();
+    summa_info().oom_splits++;
+    const int64_t h = B.n / 2;
+    for (int k = 0; k < 2; ++k) {
+      TileGuard half;
+      tile_slice_cols(B, k ? h : 0, k ? B.n : h, half.t, cs);
+      multiply_to_fn(A, half.t, sr, cs, p, off + (k ? h : 0), fn, user, cb_rc, ms, depth + 1);
+    }
+    return;
+  }
+  ms += ls.ms_symbolic + ls.ms_numeric;
+  CBG_HIP(hipStreamSynchronize(cs));
+  const int r = fn(user, p, off, &Cp.t);
+  if (r && !cb_rc) cb_rc = r;
 }
 
 static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
@@ -591,17 +696,17 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
                          Bp.t, cs);
         Buse = &Bp.t;
       }
-      TileGuard Cp;
-      LocalStats ls;
-      local_spgemm(*Ause, *Buse, sr, Cp.t, cs, &ls, arena.get());
-      panel_ms += ls.ms_symbolic + ls.ms_numeric;
-      for (auto& t : Bc[p]) tile_free_device(t.t);
-      tile_free_device(own[p].t);
       if (fn) {
-        CBG_HIP(hipStreamSynchronize(cs));
-        const int r = fn(user, p, cuts[p], &Cp.t);
-        if (r && !cb_rc) cb_rc = r;
+        multiply_to_fn(*Ause, *Buse, sr, cs, p, cuts[p], fn, user, cb_rc, panel_ms, 0);
+        for (auto& t : Bc[p]) tile_free_device(t.t);
+        tile_free_device(own[p].t);
       } else {
+        TileGuard Cp;
+        LocalStats ls;
+        local_spgemm(*Ause, *Buse, sr, Cp.t, cs, &ls, arena.get());
+        panel_ms += ls.ms_symbolic + ls.ms_numeric;
+        for (auto& t : Bc[p]) tile_free_device(t.t);
+        tile_free_device(own[p].t);
         outv.push_back(Cp.t);
         outs.push_back(std::move(Cp));
       }
@@ -613,7 +718,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     if (!g->broken) wait_comm(g);  // posted broadcasts complete before their buffers are released
     return rc;
   }
-  if (fn) return cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK;
+  if (fn) return agree(g, cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK);
   rc = step([&] {
     if (np == 1) {
       *C = outs[0].release();
@@ -672,9 +777,17 @@ static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
       st.push_back({lo, hi, sa, sb});
     }
   const int S = (int)st.size();
+  // the stage slices below assume the block layout (SpParMat::Owner): my A
+  // tile holds inner columns blk(K, pc, pcol) .. blk(K, pc, pcol + 1) and my
+  // B tile the same rows of B's row blocks; a tile of another width would be
+  // cut past its end or lose columns, so it is a dimension mismatch (agreed)
+  const bool layout_ok = A.n == blk(K, pc, g->pcol + 1) - blk(K, pc, g->pcol) &&
+                         B.m == blk(K, pr, g->prow + 1) - blk(K, pr, g->prow);
+  int rc = agree(g, layout_ok ? CBG_OK : CBG_ERR_DIMMISMATCH);
+  if (rc) return rc;
   // my pieces: A columns of the stages rooted at my grid column, B rows of those rooted at my grid row
   std::vector<TileGuard> myA(S), myB(S);
-  int rc = step([&] {
+  rc = step([&] {
     for (int s = 0; s < S; ++s) {
       if (st[s].sa == g->pcol) {
         const int64_t o = blk(K, pc, st[s].sa);
@@ -764,19 +877,23 @@ static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
 // piece small (its broadcast is exposed), the rest behind its multiply.
 // CBG_PIPELINE=k: k equal pieces (1 = no pipelining); CBG_PIPELINE=1/d: two
 // pieces, the first 1/d of B's columns; default: 1 piece without
-// communication (one grid cell), else 1/8
-static std::vector<int64_t> pipeline_cuts(cbg_grid* g, int64_t n) {
+// communication (one grid cell), else 1/8.
+// The piece COUNT is a collective property (one broadcast group and one
+// agree() per piece), so it is chosen from n_min, the narrowest B tile of the
+// world (agreed by the caller): every rank cuts its own B tile into the same
+// number of nonempty pieces, whatever the widths of the grid's column blocks.
+static std::vector<int64_t> pipeline_cuts(cbg_grid* g, int64_t n, int64_t n_min) {
   static const char* e = getenv("CBG_PIPELINE");
   const bool comm = g->pr * g->pc > 1;
-  if (n < 16) return {0, n};
+  if (n_min < 16) return {0, n};
   if (!e) return comm ? std::vector<int64_t>{0, n / 8, n} : std::vector<int64_t>{0, n};
   if (!strncmp(e, "1/", 2)) {
-    const int d = std::max(2, atoi(e + 2));
+    const int64_t d = std::min<int64_t>(std::max(2, atoi(e + 2)), n_min);
     return {0, n / d, n};
   }
   int k = atoi(e);
   if (k <= 1) return {0, n};
-  k = (int)std::min<int64_t>(k, n);
+  k = (int)std::min<int64_t>(k, n_min);
   std::vector<int64_t> c;
   for (int i = 0; i <= k; ++i) c.push_back((int64_t)i * n / k);
   return c;
@@ -789,17 +906,118 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
                  int exec, cbg_tile& C) {
   check_usable(g);
   arm_fault(g);
-  // CheckSpGEMMCompliance (ParFriends.h:160-183), agreed over the grid
+  // CheckSpGEMMCompliance (ParFriends.h:160-183), agreed over the grid, with
+  // the narrowest B tile of the world (the pipeline's piece count)
   int rc = A_gncol != B_gnrow ? CBG_ERR_DIMMISMATCH
            : (&A == &B || (A.ir == B.ir && A.nnz > 0)) ? CBG_ERR_MATRIXALIAS
            : CBG_OK;
-  if ((rc = agree(g, rc))) return rc;
+  int64_t n_min = 0;
+  if ((rc = agree_val(g, rc, B.n, &n_min, nullptr))) return rc;
   if (exec == CBG_EXEC_PANEL) {
-    // every rank cuts its B tile at the same relative places (tiles of one grid column share n)
     const bool adaptive = !getenv("CBG_PIPELINE") && g->pr * g->pc > 1;
-    return summa_panel(g, A, B, A_gncol, B_gnrow, sr, pipeline_cuts(g, B.n), nullptr, nullptr, &C, adaptive);
+    return summa_panel(g, A, B, A_gncol, B_gnrow, sr, pipeline_cuts(g, B.n, n_min), nullptr, nullptr, &C, adaptive);
   }
   return summa_staged(g, A, B, A_gncol, B_gnrow, sr, algo, C);
+}
+
+// ---------------------------------------------------------------------------
+// MemEfficientSpGEMM's phase count from memory (ParFriends.h:482-535, with
+// EstPerProcessNnzSUMMA :1243-1341).  The reference estimates this rank's
+// unmerged nnz(C) by a symbolic SUMMA (every tile broadcast once more) and
+// divides the memory left after the inputs.  Here:
+//  * flops of this rank's product C(prow, pcol) = sum over the inner index k
+//    of nnz(A(:,k) in my grid row) * nnz(B(k,:) in my grid column), from the
+//    column counts of A's tiles (allgathered along the grid row) and the row
+//    counts of B's tiles (along the grid column): count vectors, not tiles;
+//  * nnz(C) <= flops; on one rank the compression nnz/flops is measured by an
+//    exact symbolic of every 64th nonempty column of B (~1/64 of a symbolic
+//    pass) and the estimate is flops x ratio x 1.1;
+//  * the C bytes a phase may take: CBG_PHASE_MEM_FRAC (0.5) of the memory left
+//    after the tiles the SUMMA gathers -- perProcessMemory (GB, like the
+//    reference) when given, else the device's free memory plus libcbg's pool
+//    cache -- which leaves room for the symbolic bitmaps (<= 1/4 of the free
+//    memory) and the per-column arrays;
+//  * phases = ceil(12 B x nnz_est / budget), the maximum over the world (the
+//    pieces are broadcast collectively), at most the narrowest B tile's width.
+// A phase that still does not fit is split in column halves by multiply_to_fn.
+// ---------------------------------------------------------------------------
+PhasePlan& phase_plan() {
+  static thread_local PhasePlan p;
+  return p;
+}
+
+static double phase_mem_frac() {
+  static const char* e = getenv("CBG_PHASE_MEM_FRAC");
+  const double f = e ? atof(e) : 0.5;
+  return f > 0 && f <= 1 ? f : 0.5;
+}
+
+static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t K, int64_t mem_gb, int64_t n_min,
+                       int fallback, int& phases) {
+  hipStream_t cs = g->compute;
+  const int pr = g->pr, pc = g->pc;
+  // widths of A's tiles along my grid row and heights of B's along my grid column
+  std::vector<int64_t> WA(pc), HB(pr);
+  allgather_i64(g, COMM_ROW, &A.n, WA.data(), 1);
+  allgather_i64(g, COMM_COL, &B.m, HB.data(), 1);
+  int64_t wmax = 0, hmax = 0, sa = 0, sb = 0;
+  for (auto w : WA) wmax = std::max(wmax, w), sa += w;
+  for (auto h : HB) hmax = std::max(hmax, h), sb += h;
+  int rc = agree(g, (sa != K || sb != K) ? CBG_ERR_DIMMISMATCH : CBG_OK);
+  if (rc) return rc;
+  // the count vectors, padded to the widest tile, gathered on the device
+  DBuf<int32_t> ca(std::max<int64_t>(wmax, 1)), rb(std::max<int64_t>(hmax, 1));
+  DBuf<int32_t> CA(std::max<int64_t>(wmax * pc, 1)), RB(std::max<int64_t>(hmax * pr, 1));
+  rc = agree(g, step([&] { tile_counts_device(A, 0, ca.p, wmax, cs), tile_counts_device(B, 1, rb.p, hmax, cs); }));
+  if (rc) return rc;
+  allgather_device(g, COMM_ROW, ca.p, CA.p, sizeof(int32_t) * wmax);
+  allgather_device(g, COMM_COL, rb.p, RB.p, sizeof(int32_t) * hmax);
+  int64_t flops = 0;
+  rc = agree(g, step([&] {
+    std::vector<int64_t> aoff(pc + 1, 0), boff(pr + 1, 0);
+    for (int s = 0; s < pc; ++s) aoff[s + 1] = aoff[s] + WA[s];
+    for (int s = 0; s < pr; ++s) boff[s + 1] = boff[s] + HB[s];
+    flops = blocked_dot_device(CA.p, wmax, aoff, RB.p, hmax, boff, K, cs);
+  }));
+  if (rc) return rc;
+  // compression ratio from a column sample (one rank: no broadcast needed)
+  double ratio = 1.0;
+  if (g->nranks == 1 && flops > 0) {
+    static const char* es = getenv("CBG_PHASE_SAMPLE");
+    const int stride = es ? std::max(1, atoi(es)) : 64;
+    rc = step([&] {
+      TileGuard Bs;
+      tile_sample_cols(B, stride, Bs.t, cs);
+      int64_t f = 0, z = 0;
+      local_symbolic(A, Bs.t, cs, &f, &z);
+      if (f > 0) ratio = std::min(1.0, 1.1 * (double)z / (double)f);
+    });
+    if ((rc = agree(g, rc))) return rc;
+  }
+  // memory left for C after the tiles the SUMMA gathers (mine are already held)
+  auto tbytes = [](const cbg_tile& t) { return (double)(8 * (t.nzc + 1) + 4 * t.nzc + 12 * t.nnz); };
+  const double gathered = (pc - 1) * tbytes(A) + (pr - 1) * tbytes(B);
+  double avail;
+  if (mem_gb > 0) {
+    avail = (double)mem_gb * 1e9 - tbytes(A) - tbytes(B) - gathered;
+  } else {
+    size_t fr = 0, tot = 0;
+    CBG_HIP(hipMemGetInfo(&fr, &tot));
+    avail = (double)fr + (double)pool().bytes_cached() - gathered;
+  }
+  const double budget = phase_mem_frac() * avail;
+  const double need = 12.0 * ratio * (double)flops;
+  int64_t want = budget > 0 ? (int64_t)std::ceil(need / budget) : fallback;  // the reference keeps the given phases
+  want = std::max<int64_t>(1, std::min<int64_t>(want, std::max<int64_t>(1, n_min)));
+  int64_t agreed = 0;
+  if ((rc = agree_val(g, CBG_OK, want, nullptr, &agreed))) return rc;
+  phases = (int)agreed;
+  PhasePlan& pp = phase_plan();
+  pp.automatic = 1;
+  pp.flops = flops;
+  pp.nnz_est = (int64_t)(ratio * (double)flops);
+  pp.c_budget_bytes = budget;
+  return CBG_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -811,33 +1029,46 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 // one phase, so the result is identical to the unphased product.  PANEL: the
 // phases are the pipeline's pieces (A's row panel is gathered once, phase
 // p+1's B pieces are broadcast while phase p multiplies); STAGED: one staged
-// SUMMA per phase.
+// SUMMA per phase.  phases <= 0 or mem_gb > 0: the count comes from
+// plan_phases (perProcessMemory, ParFriends.h:482-535).
 // ---------------------------------------------------------------------------
 int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
-                        int algo, int exec, int phases, cbg_phase_fn fn, void* user, cbg_tile* C) {
+                        int algo, int exec, int phases, int64_t mem_gb, cbg_phase_fn fn, void* user, cbg_tile* C) {
   check_usable(g);
   arm_fault(g);
-  if (phases < 1 || phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
-  int rc = B.n < phases ? CBG_ERR_INVALIDPARAMS : CBG_OK;  // ColSplit: "Matrix is too small to be splitted"
-  if (A_gncol != B_gnrow) rc = CBG_ERR_DIMMISMATCH;
-  if ((rc = agree(g, rc))) return rc;
+  phase_plan() = PhasePlan{};
+  const bool automatic = phases <= 0 || mem_gb > 0;
+  if (!automatic && phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
+  int rc = A_gncol != B_gnrow ? CBG_ERR_DIMMISMATCH : CBG_OK;
+  int64_t n_min = 0;
+  if ((rc = agree_val(g, rc, B.n, &n_min, nullptr))) return rc;
+  if (automatic && (rc = plan_phases(g, A, B, A_gncol, mem_gb, n_min, std::max(1, phases), phases))) return rc;
+  phase_plan().phases = phases;
+  if ((rc = agree(g, B.n < phases ? CBG_ERR_INVALIDPARAMS : CBG_OK))) return rc;  // ColSplit: "Matrix is too small to be splitted"
   hipStream_t cs = g->compute;
-  // the reference copies B first, so A and B may alias here (ParFriends.h:547-549)
-  const bool alias = (&A == &B) || (A.ir == B.ir && A.nnz > 0);
   const int64_t w = B.n / phases;
   std::vector<int64_t> cuts;
   for (int p = 0; p < phases; ++p) cuts.push_back((int64_t)p * w);
   cuts.push_back(B.n);
   if (exec == CBG_EXEC_PANEL) {
+    // the reference copies B first, so A and B may alias here (ParFriends.h:547-549);
+    // the copy is a step of every rank (a no-op where they do not alias), so
+    // an empty tile on one rank cannot skip an agree() its peers make
+    const bool alias = (&A == &B) || (A.ir == B.ir && A.nnz > 0);
     TileGuard Bcopy;
-    const cbg_tile* Bu = &B;
-    if (alias) {
-      rc = step([&] { tile_slice_cols(B, 0, B.n, Bcopy.t, cs); });
-      if ((rc = agree(g, rc))) return rc;
-      Bu = &Bcopy.t;
-    }
+    rc = step([&] {
+      if (alias) tile_slice_cols(B, 0, B.n, Bcopy.t, cs);
+    });
+    if ((rc = agree(g, rc))) return rc;
     summa_info() = SummaInfo{};
-    return summa_panel(g, A, *Bu, A_gncol, B_gnrow, sr, cuts, fn, user, C);
+    const cbg_tile& Bu = alias ? Bcopy.t : B;
+    if (phases == 1) {
+      // one phase is Mult_AnXBn_DoubleBuff: B's block column arrives in the
+      // (adaptive) pipeline's pieces, each handed to fn at its column offset
+      const bool adaptive = !getenv("CBG_PIPELINE") && g->pr * g->pc > 1;
+      return summa_panel(g, A, Bu, A_gncol, B_gnrow, sr, pipeline_cuts(g, Bu.n, n_min), fn, user, C, adaptive);
+    }
+    return summa_panel(g, A, Bu, A_gncol, B_gnrow, sr, cuts, fn, user, C);
   }
   std::vector<TileGuard> parts;
   std::vector<cbg_tile> pv;
@@ -849,15 +1080,18 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
     rc = summa_staged(g, A, piece.t, A_gncol, B_gnrow, sr, algo, Cp.t);
     if (rc) return rc;
     if (fn) {
-      CBG_HIP(hipStreamSynchronize(cs));
-      const int r = fn(user, p, cuts[p], &Cp.t);
-      if (r && !cb_rc) cb_rc = r;
+      rc = step([&] {
+        CBG_HIP(hipStreamSynchronize(cs));
+        const int r = fn(user, p, cuts[p], &Cp.t);
+        if (r && !cb_rc) cb_rc = r;
+      });
+      if ((rc = agree(g, rc))) return rc;
     } else {
       pv.push_back(Cp.t);
       parts.push_back(std::move(Cp));
     }
   }
-  if (fn) return cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK;
+  if (fn) return agree(g, cb_rc ? CBG_ERR_INVALIDPARAMS : CBG_OK);
   rc = step([&] {
     if (pv.size() == 1) {
       *C = parts[0].release();
@@ -877,8 +1111,9 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
 // ---------------------------------------------------------------------------
 int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
   check_usable(g);
-  if (g->pr != g->pc) return CBG_ERR_NOTSQUARE;
+  if (g->pr != g->pc) return CBG_ERR_NOTSQUARE;  // the grid's shape: the same answer on every rank
   hipStream_t cs = g->compute;
+  const bool inject = redist_fault(g);
   // essentials of every rank's tile (world allgather: collective, diagonal ranks too)
   int64_t e[4] = {T.m, T.n, T.nnz, T.nzc};
   std::vector<int64_t> E((size_t)4 * g->nranks);
@@ -886,51 +1121,57 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
   const bool diag = g->prow == g->pcol;
   const int peer = g->pcol * g->pc + g->prow;
   const int64_t* pe = &E[4 * (size_t)peer];
-  cbg_tile R{};
-  if (!diag) tile_alloc_device(R, pe[0], pe[1], pe[2], pe[3]);
-  if (g->host_mode && g->nranks > 1) {
-    // every off-diagonal rank broadcasts its tile over the world communicator
-    for (int q = 0; q < g->nranks; ++q) {
-      const int qr = q / g->pc, qc = q % g->pc;
-      if (qr == qc) continue;
-      const int64_t* qe = &E[4 * (size_t)q];
-      const bool mine = q == g->rank, keep = !diag && q == peer;
-      auto hb = [&](void* dst, const void* src, size_t bytes) {
-        if (bytes == 0) return;
-        std::vector<char> h(bytes);
-        if (mine) CBG_HIP(hipMemcpy(h.data(), src, bytes, hipMemcpyDeviceToHost));
-        host_check(g, g->hc.bcast(g->hc.user, COMM_WORLD, h.data(), bytes, q), "transpose bcast");
-        if (keep) CBG_HIP(hipMemcpy(dst, h.data(), bytes, hipMemcpyHostToDevice));
-      };
-      hb(R.cp, T.cp, sizeof(int64_t) * (qe[3] + 1));
-      hb(R.jc, T.jc, sizeof(int32_t) * qe[3]);
-      hb(R.ir, T.ir, sizeof(int32_t) * qe[2]);
-      hb(R.val, T.val, sizeof(double) * qe[2]);
+  // every rank holds its receive buffer before anyone sends (agreed)
+  TileGuard R;
+  int rc = step([&] {
+    if (inject) throw HipError("injected fault (CBG_FAULT_INJECT_REDIST) in Transpose", CBG_ERR_OOM);
+    if (!diag) tile_alloc_device(R.t, pe[0], pe[1], pe[2], pe[3]);
+  });
+  if ((rc = agree(g, rc))) return rc;
+  int local = step([&] {
+    if (g->host_mode && g->nranks > 1) {
+      // every off-diagonal rank broadcasts its tile over the world communicator
+      for (int q = 0; q < g->nranks; ++q) {
+        const int qr = q / g->pc, qc = q % g->pc;
+        if (qr == qc) continue;
+        const int64_t* qe = &E[4 * (size_t)q];
+        const bool mine = q == g->rank, keep = !diag && q == peer;
+        auto hb = [&](void* dst, const void* src, size_t bytes) {
+          if (bytes == 0) return;
+          std::vector<char> h(bytes);
+          if (mine) CBG_HIP(hipMemcpy(h.data(), src, bytes, hipMemcpyDeviceToHost));
+          host_check(g, g->hc.bcast(g->hc.user, COMM_WORLD, h.data(), bytes, q), "transpose bcast");
+          if (keep) CBG_HIP(hipMemcpy(dst, h.data(), bytes, hipMemcpyHostToDevice));
+        };
+        hb(R.t.cp, T.cp, sizeof(int64_t) * (qe[3] + 1));
+        hb(R.t.jc, T.jc, sizeof(int32_t) * qe[3]);
+        hb(R.t.ir, T.ir, sizeof(int32_t) * qe[2]);
+        hb(R.t.val, T.val, sizeof(double) * qe[2]);
+      }
+    } else if (!diag) {
+      ncclComm_t c = g->world;
+      CBG_NCCL(ncclGroupStart());
+      CBG_NCCL(ncclSend(T.cp, T.nzc + 1, ncclInt64, peer, c, g->comm));
+      CBG_NCCL(ncclRecv(R.t.cp, pe[3] + 1, ncclInt64, peer, c, g->comm));
+      if (T.nzc) CBG_NCCL(ncclSend(T.jc, T.nzc, ncclInt32, peer, c, g->comm));
+      if (pe[3]) CBG_NCCL(ncclRecv(R.t.jc, pe[3], ncclInt32, peer, c, g->comm));
+      if (T.nnz) {
+        CBG_NCCL(ncclSend(T.ir, T.nnz, ncclInt32, peer, c, g->comm));
+        CBG_NCCL(ncclSend(T.val, T.nnz, ncclFloat64, peer, c, g->comm));
+      }
+      if (pe[2]) {
+        CBG_NCCL(ncclRecv(R.t.ir, pe[2], ncclInt32, peer, c, g->comm));
+        CBG_NCCL(ncclRecv(R.t.val, pe[2], ncclFloat64, peer, c, g->comm));
+      }
+      CBG_NCCL(ncclGroupEnd());
+      wait_comm(g);
     }
-  } else if (!diag) {
-    ncclComm_t c = g->world;
-    CBG_NCCL(ncclGroupStart());
-    CBG_NCCL(ncclSend(T.cp, T.nzc + 1, ncclInt64, peer, c, g->comm));
-    CBG_NCCL(ncclRecv(R.cp, pe[3] + 1, ncclInt64, peer, c, g->comm));
-    if (T.nzc) CBG_NCCL(ncclSend(T.jc, T.nzc, ncclInt32, peer, c, g->comm));
-    if (pe[3]) CBG_NCCL(ncclRecv(R.jc, pe[3], ncclInt32, peer, c, g->comm));
-    if (T.nnz) {
-      CBG_NCCL(ncclSend(T.ir, T.nnz, ncclInt32, peer, c, g->comm));
-      CBG_NCCL(ncclSend(T.val, T.nnz, ncclFloat64, peer, c, g->comm));
-    }
-    if (pe[2]) {
-      CBG_NCCL(ncclRecv(R.ir, pe[2], ncclInt32, peer, c, g->comm));
-      CBG_NCCL(ncclRecv(R.val, pe[2], ncclFloat64, peer, c, g->comm));
-    }
-    CBG_NCCL(ncclGroupEnd());
-    wait_comm(g);
-  }
-  if (diag) {
-    tile_transpose(T, out, cs);
-  } else {
-    tile_transpose(R, out, cs);
-    tile_free_device(R);
-  }
+  });
+  // the local transpose (SpDCCols::Transpose) only where the exchange worked
+  TileGuard O;
+  if (!local) local = step([&] { tile_transpose(diag ? T : R.t, O.t, cs); });
+  if ((rc = agree(g, local))) return rc;
+  out = O.release();
   return CBG_OK;
 }
 
@@ -942,7 +1183,9 @@ int grid_transpose(cbg_grid* g, const cbg_tile& T, cbg_tile& out) {
 // SpParMat.cpp:5068-5097).  Rows only move inside a grid column (columns
 // inside a grid row): every rank broadcasts its slice of the range to its
 // column (row) communicator and keeps the part of each slice that falls in
-// its new block.
+// its new block.  Collective steps agree on a code like the SUMMA's: a rank
+// that cannot allocate a receive buffer makes every rank return the code
+// before any of them posts the broadcast it would have skipped.
 // ---------------------------------------------------------------------------
 int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, int dim, int64_t lo, int64_t hi,
                        cbg_tile& out) {
@@ -951,6 +1194,7 @@ int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, i
   const int64_t gext = dim == 0 ? gm : gn;
   if (lo < 0 || hi < lo || hi > gext) return CBG_ERR_INVALIDPARAMS;
   hipStream_t cs = g->compute;
+  const bool inject = redist_fault(g);
   const int which = dim == 0 ? COMM_COL : COMM_ROW;
   const int np = comm_size(g, which), me = comm_rank(g, which);
   // my old range [S0, S1) along dim and my new range [lo + T0, lo + T1)
@@ -965,56 +1209,71 @@ int grid_block_extract(cbg_grid* g, const cbg_tile& T, int64_t gm, int64_t gn, i
   T0 += lo;
   T1 += lo;
   auto cut = [&](const cbg_tile& X, int64_t a, int64_t b, cbg_tile& piece) {  // local range [a, b) of X
-    cbg_tile head{}, rest{}, tail{};
+    TileGuard head, rest, tail;
     if (dim == 0) {
-      tile_split_rows(X, b, head, tail, cs);
-      tile_free_device(tail);
-      tile_split_rows(head, a, rest, piece, cs);
+      tile_split_rows(X, b, head.t, tail.t, cs);
+      tail = TileGuard();
+      tile_split_rows(head.t, a, rest.t, piece, cs);
     } else {
-      tile_split_cols(X, b, head, tail, cs);
-      tile_free_device(tail);
-      tile_split_cols(head, a, rest, piece, cs);
+      tile_split_cols(X, b, head.t, tail.t, cs);
+      tail = TileGuard();
+      tile_split_cols(head.t, a, rest.t, piece, cs);
     }
-    tile_free_device(rest);
-    tile_free_device(head);
   };
   // my slice of [lo, hi)
   const int64_t x0 = std::max(S0, lo), x1 = std::max(x0, std::min(S1, hi));
-  cbg_tile mine{};
-  cut(T, x0 - S0, x1 - S0, mine);
-  int64_t e[4] = {mine.m, mine.n, mine.nnz, mine.nzc};
+  TileGuard mine;
+  int rc = step([&] { cut(T, x0 - S0, x1 - S0, mine.t); });
+  int64_t e[4] = {mine.t.m, mine.t.n, mine.t.nnz, mine.t.nzc};
+  if (rc) e[0] = e[1] = e[2] = e[3] = 0;
+  if ((rc = agree(g, rc))) return rc;
   std::vector<int64_t> E((size_t)4 * np);
   allgather_i64(g, which, e, E.data(), 4);
-  std::vector<cbg_tile> parts;
+  std::vector<TileGuard> parts;
   std::vector<int64_t> offs;
+  int local = CBG_OK;
   for (int q = 0; q < np; ++q) {
     int64_t Q0, Q1;
     span(gext, np, q, Q0, Q1);
     const int64_t y0 = std::max(Q0, lo), y1 = std::max(y0, std::min(Q1, hi));  // slice of rank q
-    cbg_tile sl = q == me ? mine : cbg_tile{};
-    if (q != me) alloc_like(sl, &E[4 * (size_t)q]);
-    bcast_group(g, [&] { bcast_tile(g, which, q, &E[4 * (size_t)q], sl, q == me); });
-    wait_comm(g);
+    TileGuard recv;
+    rc = step([&] {
+      if (inject && q == (me + 1) % np) throw HipError("injected fault (CBG_FAULT_INJECT_REDIST) in BlockSplit", CBG_ERR_OOM);
+      if (q != me) alloc_like(recv.t, &E[4 * (size_t)q]);
+    });
+    if ((rc = agree(g, rc))) return rc;  // every receive buffer of this broadcast exists
+    cbg_tile& sl = q == me ? mine.t : recv.t;
+    local = std::max(local, step([&] {
+      bcast_group(g, [&] { bcast_tile(g, which, q, &E[4 * (size_t)q], sl, q == me); });
+      wait_comm(g);
+    }));
     const int64_t z0 = std::max(y0, T0), z1 = std::min(y1, T1);  // the part of it in my new range
-    if (z1 > z0) {
-      cbg_tile piece{};
-      cut(sl, z0 - y0, z1 - y0, piece);
-      parts.push_back(piece);
-      offs.push_back(z0 - T0);
-    }
-    if (q != me) tile_free_device(sl);
+    if (!local && z1 > z0)
+      local = step([&] {
+        TileGuard piece;
+        cut(sl, z0 - y0, z1 - y0, piece.t);
+        parts.push_back(std::move(piece));
+        offs.push_back(z0 - T0);
+      });
   }
-  tile_free_device(mine);
+  mine = TileGuard();
   const int64_t om = dim == 0 ? T1 - T0 : T.m, on = dim == 0 ? T.n : T1 - T0;
-  if (parts.empty()) {
-    tile_alloc_device(out, om, on, 0, 0);
-  } else if (dim == 0) {
-    tile_concat_rows(parts, offs, om, on, out, cs);
-  } else {
-    tile_concat_cols(parts, offs, om, on, out, cs);
-  }
-  for (auto& t : parts) tile_free_device(t);
-  CBG_HIP(hipStreamSynchronize(cs));
+  TileGuard O;
+  if (!local)
+    local = step([&] {
+      std::vector<cbg_tile> pv;
+      for (auto& t : parts) pv.push_back(t.t);
+      if (pv.empty()) {
+        tile_alloc_device(O.t, om, on, 0, 0);
+      } else if (dim == 0) {
+        tile_concat_rows(pv, offs, om, on, O.t, cs);
+      } else {
+        tile_concat_cols(pv, offs, om, on, O.t, cs);
+      }
+      CBG_HIP(hipStreamSynchronize(cs));
+    });
+  if ((rc = agree(g, local))) return rc;
+  out = O.release();
   return CBG_OK;
 }
 

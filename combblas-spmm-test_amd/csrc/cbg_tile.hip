@@ -832,4 +832,108 @@ bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s)
   return h == 0;
 }
 
+// ---------------------------------------------------------------------------
+// phase planning (MemEfficientSpGEMM's memory-driven phase count,
+// ParFriends.h:482-535): the flops of a SUMMA product from the column counts
+// of A's tiles and the row counts of B's tiles, and a column sample of B for
+// the compression ratio
+// ---------------------------------------------------------------------------
+__global__ void k_col_counts(int64_t nzc, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
+                             int32_t* __restrict__ cnt) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < nzc) cnt[jc[i]] = (int32_t)(cp[i + 1] - cp[i]);
+}
+__global__ void k_row_counts(int64_t nnz, const int32_t* __restrict__ ir, int32_t* __restrict__ cnt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[ir[i]], 1);
+}
+void tile_counts_device(const cbg_tile& t, int dim, int32_t* d, int64_t padded, hipStream_t s) {
+  if (padded > 0) CBG_HIP(hipMemsetAsync(d, 0, sizeof(int32_t) * padded, s));
+  if (dim == 0 && t.nzc > 0)
+    hipLaunchKernelGGL(k_col_counts, dim3((unsigned)((t.nzc + 255) / 256)), dim3(256), 0, s, t.nzc, t.cp, t.jc, d);
+  if (dim == 1 && t.nnz > 0)
+    hipLaunchKernelGGL(k_row_counts, dim3((unsigned)std::min<int64_t>((t.nnz + 255) / 256, 8192)), dim3(256), 0, s,
+                       t.nnz, t.ir, d);
+  CBG_HIP(hipStreamSynchronize(s));  // the comm stream reads the counts next
+}
+
+// sum over k < K of a[k] * b[k], where a is split into segments aoff[s]..aoff[s+1]
+// stored at a + s * astride (b likewise): the inner index walks A's column
+// blocks and B's row blocks at once
+struct DotSegs {
+  int na, nb;
+  int64_t aoff[65], boff[65];
+};
+__device__ __forceinline__ int seg_of_k(const int64_t* off, int n, int64_t k) {
+  int s = 0;
+  while (s + 1 < n && off[s + 1] <= k) ++s;
+  return s;
+}
+__global__ void k_blocked_dot(const int32_t* __restrict__ a, int64_t astride, const int32_t* __restrict__ b,
+                              int64_t bstride, DotSegs sg, int64_t K, unsigned long long* __restrict__ out) {
+  unsigned long long acc = 0;
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
+    const int sa = seg_of_k(sg.aoff, sg.na, k), sb = seg_of_k(sg.boff, sg.nb, k);
+    acc += (unsigned long long)a[sa * astride + (k - sg.aoff[sa])] * (unsigned long long)b[sb * bstride + (k - sg.boff[sb])];
+  }
+  acc = (unsigned long long)wave_sum64((long long)acc);
+  if (lane_id() == 0 && acc) atomicAdd(out, acc);
+}
+int64_t blocked_dot_device(const int32_t* a, int64_t astride, const std::vector<int64_t>& aoff, const int32_t* b,
+                           int64_t bstride, const std::vector<int64_t>& boff, int64_t K, hipStream_t s) {
+  DotSegs sg{};
+  if (aoff.size() > 65 || boff.size() > 65) throw HipError("phase plan: grid dimension above 64", CBG_ERR_NOTSUPPORTED);
+  sg.na = (int)aoff.size() - 1;
+  sg.nb = (int)boff.size() - 1;
+  for (size_t i = 0; i < aoff.size(); ++i) sg.aoff[i] = aoff[i];
+  for (size_t i = 0; i < boff.size(); ++i) sg.boff[i] = boff[i];
+  DBuf<unsigned long long> d(1);
+  CBG_HIP(hipMemsetAsync(d.p, 0, sizeof(unsigned long long), s));
+  if (K > 0)
+    hipLaunchKernelGGL(k_blocked_dot, dim3((unsigned)std::min<int64_t>((K + 255) / 256, 4096)), dim3(256), 0, s, a,
+                       astride, b, bstride, sg, K, d.p);
+  unsigned long long h = 0;
+  CBG_HIP(hipMemcpyAsync(&h, d.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  return (int64_t)h;
+}
+
+// every stride-th nonempty column (DCSC positions 0, stride, 2 stride, ...) of T,
+// same shape and column ids: a wave per sampled column copies its entries
+__global__ void k_sample_len(int64_t ns, int stride, const int64_t* __restrict__ cp, int64_t* __restrict__ len) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < ns) len[i] = cp[i * stride + 1] - cp[i * stride];
+}
+__global__ void k_sample_copy(int64_t ns, int stride, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
+                              const int32_t* __restrict__ ir, const double* __restrict__ val,
+                              const int64_t* __restrict__ ocp, int32_t* __restrict__ ojc, int32_t* __restrict__ oir,
+                              double* __restrict__ oval) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  if (i >= ns) return;
+  const int64_t src = cp[i * stride], n = cp[i * stride + 1] - src, dst = ocp[i];
+  if (lane_id() == 0) ojc[i] = jc[i * stride];
+  for (int64_t q = lane_id(); q < n; q += WAVE) {
+    oir[dst + q] = ir[src + q];
+    oval[dst + q] = val[src + q];
+  }
+}
+void tile_sample_cols(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s) {
+  const int64_t ns = T.nzc > 0 ? (T.nzc + stride - 1) / stride : 0;
+  if (ns == 0) {
+    tile_alloc_device(out, T.m, T.n, 0, 0);
+    return;
+  }
+  DBuf<int64_t> len(ns + 1), off(ns + 1);
+  hipLaunchKernelGGL(k_sample_len, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, ns, stride, T.cp, len.p);
+  exclusive_scan_i64(len.p, off.p, ns, s);
+  int64_t nnz = 0;
+  CBG_HIP(hipMemcpyAsync(&nnz, off.p + ns, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  tile_alloc_device(out, T.m, T.n, nnz, ns);
+  CBG_HIP(hipMemcpyAsync(out.cp, off.p, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_sample_copy, dim3((unsigned)((ns * WAVE + 255) / 256)), dim3(256), 0, s, ns, stride, T.cp, T.jc,
+                     T.ir, T.val, off.p, out.jc, out.ir, out.val);
+  CBG_HIP(hipStreamSynchronize(s));
+}
+
 }  // namespace cbg

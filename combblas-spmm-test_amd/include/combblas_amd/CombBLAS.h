@@ -687,8 +687,11 @@ SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, UDERA>& A, SpParMat<
 }
 // ParFriends.h:449-451 signature.  Phases cut B's local tile by columns and C is
 // column-concatenated; the Markov-clustering pruning arguments must keep their
-// no-pruning values (hardThreshold, selectNum, recoverNum, recoverPct <= 0),
-// kselectVersion/computationKernel/perProcessMemory are accepted and unused.
+// no-pruning values (hardThreshold, selectNum, recoverNum, recoverPct <= 0);
+// perProcessMemory > 0 (GB) picks the phase count from memory like the
+// reference (ParFriends.h:482-535; see cbg_summa_spgemm_memeff), phases < 1 is
+// reset to 1 (:469-473); kselectVersion/computationKernel select CPU kernels of
+// the reference and are unused here.
 template <typename SR, typename NUO, typename UDERO, typename IU, typename NU1, typename NU2, typename UDERA,
           typename UDERB>
 SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B, int phases,
@@ -696,14 +699,14 @@ SpParMat<IU, NUO, UDERO> MemEfficientSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMa
                                              int kselectVersion, int computationKernel, int64_t perProcessMemory) {
   (void)kselectVersion;
   (void)computationKernel;
-  (void)perProcessMemory;
   if (hardThreshold > 0 || selectNum > 0 || recoverNum > 0 || recoverPct > 0)
     cbg_abort_on(CBG_ERR_INVALIDPARAMS, "MemEfficientSpGEMM: pruning is not supported");
   if (A.getncol() != B.getnrow()) cbg_abort_on(CBG_ERR_DIMMISMATCH, "Can not multiply, dimensions does not match");
+  if (phases < 1) phases = 1;
   cbg_tile c{};
-  cbg_abort_on(cbg_summa_spgemm_phased(A.commGrid->handle(), A.spSeq->tile(), B.spSeq->tile(), A.getncol(),
-                                       B.getnrow(), SR::code, CBG_DOUBLEBUFF, CBG_EXEC_PANEL, phases, nullptr,
-                                       nullptr, &c),
+  cbg_abort_on(cbg_summa_spgemm_memeff(A.commGrid->handle(), A.spSeq->tile(), B.spSeq->tile(), A.getncol(),
+                                       B.getnrow(), SR::code, CBG_DOUBLEBUFF, CBG_EXEC_PANEL, phases,
+                                       perProcessMemory > 0 ? perProcessMemory : 0, nullptr, nullptr, &c),
                "MemEfficientSpGEMM");
   return SpParMat<IU, NUO, UDERO>(new UDERO(c), A.commGrid, A.getnrow(), B.getncol());
 }

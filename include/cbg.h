@@ -219,12 +219,33 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_loc
  *               and freed after the call (C streamed when it does not fit HBM;
  *               C_local may be NULL).  fn runs on every rank between the
  *               collectives; a nonzero return is reported after all phases.
- * phases < 1 or >= A_gncol is reset to 1 (ParFriends.h:469-473).  Every rank
- * needs B_local->n >= phases (CBG_ERR_INVALIDPARAMS otherwise, collectively). */
+ * phases >= A_gncol is reset to 1 (ParFriends.h:469-473); phases <= 0 picks the
+ * count from device memory (see cbg_summa_spgemm_memeff).  Every rank needs
+ * B_local->n >= phases (CBG_ERR_INVALIDPARAMS otherwise, collectively).  With fn,
+ * a phase whose C does not fit the device after all is computed as column
+ * halves of its B piece (each handed to fn with the same phase index and its
+ * own col_offset). */
 typedef int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg_tile* C_phase);
 int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
                             int64_t B_gnrow, int semiring, int algo, int exec, int phases, cbg_phase_fn fn,
                             void* user, cbg_tile* C_local);
+/* The same with MemEfficientSpGEMM's perProcessMemory (GB, ParFriends.h:482-535):
+ * when per_process_memory_gb > 0 (or phases <= 0) the phase count comes from
+ * memory: the flops of this rank's product (from the column counts of A's tiles
+ * and the row counts of B's tiles, allgathered along the grid row / column), an
+ * nnz(C) estimate (flops, times the compression of an exact symbolic of every
+ * 64th column of B on one rank), and half of the memory left after the tiles the
+ * SUMMA gathers -- perProcessMemory, or the device's free memory when it is 0;
+ * the maximum over the grid.  If that memory is already taken by the inputs the
+ * given phases are kept, like the reference. */
+int cbg_summa_spgemm_memeff(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
+                            int64_t B_gnrow, int semiring, int algo, int exec, int phases,
+                            int64_t per_process_memory_gb, cbg_phase_fn fn, void* user, cbg_tile* C_local);
+/* the last (memeff / phased) call's phase plan: phases run, whether they were
+ * chosen from memory, this rank's product flops and estimated nnz(C), the C bytes
+ * a phase was allowed, and phases split in halves after an out-of-memory */
+int cbg_last_phase_plan(int* phases, int* automatic, int64_t* flops, int64_t* nnz_est, double* c_budget_bytes,
+                        int* oom_splits);
 
 /* SpParMat::Transpose (SpParMat.cpp:3528-3590), collective over a square grid:
  * out = this rank's tile of the transposed matrix (the transpose of the

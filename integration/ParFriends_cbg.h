@@ -1,15 +1,26 @@
 // ParFriends_cbg.h -- the adapter a CombBLAS maintainer adds next to
 // Mult_AnXBn_DoubleBuff (include/CombBLAS/ParFriends.h:798) so that the
 // reference's own drivers (MultTest, MultTiming, GalerkinNew) multiply on
-// MI355X through libcbg's C ABI (include/cbg.h).  Include it after
-// "CombBLAS/CombBLAS.h"; IT = int64_t or int.  INTEGRATION.md section 2;
-// compiled and linked against the reference headers by
-// tests/test_capi.py::test_reference_adapter_compiles (integration/adapter_check.cpp).
+// MI355X through libcbg's C ABI (include/cbg.h).  It includes
+// "CombBLAS/CombBLAS.h" itself, so a driver picks up the GPU path with this one
+// extra include (or `-include ParFriends_cbg.h` on its compile line) and no
+// other change: the explicit specializations at the end replace the
+// reference's Mult_AnXBn_DoubleBuff / Mult_AnXBn_Synch templates for the
+// concrete types the ReleaseTests instantiate (PlusTimesSRing<double,double>
+// and MinPlusSRing<double,double> on SpDCCols<int|int64_t, double>), and
+// PSpGEMM (SpParMat.h:454-467), which calls Mult_AnXBn_Synch, follows.
+// INTEGRATION.md section 2; compiled against the reference headers by
+// oracle/Makefile (adapter_check.cpp, and ReleaseTests/MultTiming.cpp unmodified).
 #pragma once
+#include <mpi.h>
+
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <tuple>
 #include <vector>
 
+#include "CombBLAS/CombBLAS.h"
 #include "cbg.h"
 
 namespace combblas {
@@ -103,5 +114,49 @@ SpParMat<IT, double, SpDCCols<IT, double>> Mult_AnXBn_Synch_cbg(SpParMat<IT, dou
                                                                  SpParMat<IT, double, SpDCCols<IT, double>>& B) {
   return Mult_AnXBn_cbg(A, B, CBG_SYNCH);
 }
+
+// ---------------------------------------------------------------------------
+// Drop-in: explicit specializations of the reference templates
+//   template<SR, NUO, UDERO, IU, NU1, NU2, UDERA, UDERB>
+//   SpParMat<IU,NUO,UDERO> Mult_AnXBn_DoubleBuff(SpParMat<IU,NU1,UDERA>&, SpParMat<IU,NU2,UDERB>&,
+//                                               bool clearA, bool clearB)   ParFriends.h:798-800
+//   ... Mult_AnXBn_Synch                                                    ParFriends.h:1004-1006
+// for the types MultTiming.cpp:58,71,83,92 / MultTest.cpp:162,173 /
+// GalerkinNew.cpp:105-152 (through PSpGEMM) instantiate.  clearA / clearB free
+// the inputs' local tiles after the multiply, like the reference (:966-993).
+// CBG_ADAPTER_VERBOSE=1 prints one line per call on rank 0 (tests).
+// ---------------------------------------------------------------------------
+template <class IT>
+static SpParMat<IT, double, SpDCCols<IT, double>> cbg_dropin(SpParMat<IT, double, SpDCCols<IT, double>>& A,
+                                                             SpParMat<IT, double, SpDCCols<IT, double>>& B,
+                                                             bool clearA, bool clearB, int algo, int semiring,
+                                                             const char* name) {
+  if (std::getenv("CBG_ADAPTER_VERBOSE") && A.getcommgrid()->GetRank() == 0)
+    std::fprintf(stderr, "[cbg adapter] %s on MI355X (libcbg), semiring %d\n", name, semiring);
+  SpParMat<IT, double, SpDCCols<IT, double>> C = Mult_AnXBn_cbg(A, B, algo, semiring);
+  if (clearA) A.FreeMemory();
+  if (clearB) B.FreeMemory();
+  return C;
+}
+
+#define CBG_DROPIN(FN, ALGO, SRT, SRCODE, IT)                                                                     \
+  template <>                                                                                                   \
+  inline SpParMat<IT, double, SpDCCols<IT, double>>                                                             \
+  FN<SRT, double, SpDCCols<IT, double>, IT, double, double, SpDCCols<IT, double>, SpDCCols<IT, double>>(          \
+      SpParMat<IT, double, SpDCCols<IT, double>> & A, SpParMat<IT, double, SpDCCols<IT, double>> & B, bool clearA, \
+      bool clearB) {                                                                                            \
+    return cbg_dropin<IT>(A, B, clearA, clearB, ALGO, SRCODE, #FN);                                            \
+  }
+#define CBG_DROPIN_ALL(IT)                                                                          \
+  CBG_DROPIN(Mult_AnXBn_DoubleBuff, CBG_DOUBLEBUFF, PlusTimesSRing<double CBG_COMMA double>, CBG_PLUS_TIMES, IT) \
+  CBG_DROPIN(Mult_AnXBn_Synch, CBG_SYNCH, PlusTimesSRing<double CBG_COMMA double>, CBG_PLUS_TIMES, IT)           \
+  CBG_DROPIN(Mult_AnXBn_DoubleBuff, CBG_DOUBLEBUFF, MinPlusSRing<double CBG_COMMA double>, CBG_MIN_PLUS, IT)     \
+  CBG_DROPIN(Mult_AnXBn_Synch, CBG_SYNCH, MinPlusSRing<double CBG_COMMA double>, CBG_MIN_PLUS, IT)
+#define CBG_COMMA ,
+CBG_DROPIN_ALL(int)
+CBG_DROPIN_ALL(int64_t)
+#undef CBG_DROPIN_ALL
+#undef CBG_DROPIN
+#undef CBG_COMMA
 
 }  // namespace combblas

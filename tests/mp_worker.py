@@ -40,6 +40,8 @@ def main():
     if case == "fault" and rank == world - 1:
         # its 2nd (PANEL) and 3rd (STAGED) SUMMA call, or the first two (CBG_FAULT_FIRST=1)
         os.environ["CBG_FAULT_INJECT"] = "%d:%s" % (rank, "0,1" if os.environ.get("CBG_FAULT_FIRST") == "1" else "1,2")
+    if case == "redist_fault" and rank == world - 1:
+        os.environ["CBG_FAULT_INJECT_REDIST"] = "%d:0,1" % rank  # its first Transpose and first BlockSplit
     if mode == "rccl":
         os.environ["NCCL_HOSTID"] = "cbg-test-rank-%d" % rank
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
@@ -257,6 +259,133 @@ def main():
         if rank == 0:
             print("MPOK" if ok else f"BLOCKSPGEMM FAILED {tot} vs {gd}", flush=True)
         return
+    if case == "narrow":
+        # B tiles of uneven, narrow widths (31 columns on a 1 x 2 grid: 15 and 16):
+        # the pipeline's piece count is agreed from the narrowest tile, so every
+        # rank makes the same collectives (CBG_PIPELINE from the test: unset, 2, 1/4)
+        from helpers import oracle_local
+        rng = np.random.default_rng(5)
+        n = 31
+        dense = (rng.random((n, n)) < 0.3) * rng.uniform(-1, 1, (n, n))
+        cols, rows = np.nonzero(dense.T)
+        H = dict(m=n, n=n, cp=np.searchsorted(cols, np.arange(n + 1)).astype(np.int64), jc=np.arange(n, dtype=np.int32),
+                 ir=rows.astype(np.int32), val=dense.T[cols, rows].astype(np.float64))
+        keep = np.diff(H["cp"]) > 0
+        H["jc"] = H["jc"][keep]
+        H["cp"] = np.append(H["cp"][:-1][keep], H["cp"][-1]).astype(np.int64)
+        from helpers import abs_tile, assert_tiles_equal
+        ref = oracle_local(H, H)
+        bound = oracle_local(abs_tile(H), abs_tile(H))
+        grid = make_grid()
+        Ad = cbg.SpParMat.from_global(grid, H)
+        Bd = cbg.SpParMat.from_global(grid, H)
+        r0, r1 = cbg.block_range(n, pr, grid.prow)
+        c0, c1 = cbg.block_range(n, pc, grid.pcol)
+        want, wb = cbg.sub_tile(ref, r0, r1, c0, c1), cbg.sub_tile(bound, r0, r1, c0, c1)
+        ok = True
+        for ex in (0, 1):
+            for f in (cbg.Mult_AnXBn_DoubleBuff, cbg.Mult_AnXBn_Synch):
+                C = f(Ad, Bd, exec_mode=ex)
+                try:
+                    assert_tiles_equal(C.tile.to_host(), want, rtol=1e-12, bound=wb["val"])
+                except AssertionError as e:
+                    print(rank, "narrow", ex, f.__name__, e, flush=True)
+                    ok = False
+                C.tile.free()
+        Cp = cbg.MemEfficientSpGEMM(Ad, Bd, 3)
+        try:
+            assert_tiles_equal(Cp.tile.to_host(), want, rtol=1e-12, bound=wb["val"])
+        except AssertionError as e:
+            print(rank, "narrow phased", e, flush=True)
+            ok = False
+        oks = hc.allgather(0, b"1" if ok else b"0")
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if oks == b"1" * world else "NARROW FAILED %r" % oks, flush=True)
+        return
+    if case == "mismatch":
+        # a tile off the block layout (the last rank's A tile one column short):
+        # PANEL and STAGED both return CBG_ERR_DIMMISMATCH on every rank, and the
+        # grid still multiplies afterwards
+        Ah = load_npz("rmat_s10_ef16_A.npz")
+        gd = G["rmat"]["s10_ef16"]["C_local_plus"]
+        grid = make_grid()
+        Ad = cbg.SpParMat.from_global(grid, Ah)
+        Bd = cbg.SpParMat.from_global(grid, Ah)
+        bad = Ad
+        if rank == world - 1:
+            left, right = Ad.tile.split_cols(Ad.tile.n - 1)
+            right.free()
+            bad = cbg.SpParMat(left, grid, Ad.gm, Ad.gn)
+        ok = True
+        for ex in (0, 1):
+            try:
+                cbg.Mult_AnXBn_DoubleBuff(bad, Bd, exec_mode=ex)
+                ok = False
+                print(rank, "no error", ex, flush=True)
+            except cbg.CbgError as e:
+                if e.code != cbg.DIMMISMATCH:
+                    ok = False
+                    print(rank, "wrong code", ex, e, flush=True)
+        C = cbg.Mult_AnXBn_DoubleBuff(Ad, Bd)
+        r0, _ = cbg.block_range(Ah["m"], pr, grid.prow)
+        c0, _ = cbg.block_range(Ah["n"], pc, grid.pcol)
+        import pickle
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(C.tile.digest(r0, c0)))))]
+        tot = add_digests(alld)
+        ok = ok and tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and tot["hv"] == gd["hv"]
+        oks = hc.allgather(0, b"1" if ok else b"0")
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if oks == b"1" * world else "MISMATCH FAILED %r" % oks, flush=True)
+        return
+    if case == "redist_fault":
+        # CBG_FAULT_INJECT_REDIST makes the last rank's first Transpose and first
+        # BlockSplit fail their receive-buffer allocation: every rank returns
+        # CBG_ERR_OOM (no rank left in a send/recv or broadcast), then both work
+        from helpers import transpose_host
+        Ah = load_npz("rmat_s10_ef16_A.npz")
+        grid = make_grid()
+        ok = True
+        for what in ("transpose", "blocksplit"):
+            X = cbg.SpParMat.from_global(grid, Ah)
+            try:
+                X.Transpose() if what == "transpose" else X.BlockSplit(3, 1)
+                ok = False
+                print(rank, what, "no error", flush=True)
+            except cbg.CbgError as e:
+                if e.code != cbg.OOM:
+                    ok = False
+                    print(rank, what, "wrong code", e, flush=True)
+            X.tile.free()
+        X = cbg.SpParMat.from_global(grid, Ah)
+        X.Transpose()
+        Th = transpose_host(Ah)
+        r0, r1 = cbg.block_range(Th["m"], pr, grid.prow)
+        c0, c1 = cbg.block_range(Th["n"], pc, grid.pcol)
+        from helpers import assert_tiles_equal
+        try:
+            assert_tiles_equal(X.tile.to_host(), cbg.sub_tile(Th, r0, r1, c0, c1))
+        except AssertionError as e:
+            ok = False
+            print(rank, "transpose after the fault", e, flush=True)
+        blocks = cbg.SpParMat.from_global(grid, Ah).BlockSplit(3, 1)
+        roff = cbg._block_offsets(Ah["m"], 3)
+        for i in range(3):
+            Xb = blocks[i][0]
+            a0, a1 = cbg.block_range(Xb.gm, pr, grid.prow)
+            b0, b1 = cbg.block_range(Xb.gn, pc, grid.pcol)
+            h = Xb.tile.to_host()
+            want = cbg.sub_tile(Ah, roff[i] + a0, roff[i] + a1, b0, b1)
+            ok = ok and all(np.array_equal(np.asarray(h[k]), np.asarray(want[k])) for k in ("cp", "jc", "ir", "val"))
+        oks = hc.allgather(0, b"1" if ok else b"0")
+        grid.destroy()
+        dist.barrier()
+        if rank == 0:
+            print("MPOK" if oks == b"1" * world else "REDIST FAULT FAILED %r" % oks, flush=True)
+        return
     if case.startswith("rmat"):
         A = load_npz("rmat_s10_ef16_A.npz")
         B = A
@@ -315,7 +444,22 @@ def main():
             if case.startswith("rmat"):
                 good = good and tot["hv"] == gd["hv"]
             else:
-                good = good and abs(tot["vsum"] - gd["vsum"]) < 1e-9 * max(1, abs(gd["vsum"]))
+                # every entry of this rank's tile within 1e-12 (|A||B|)_ij of the
+                # reference's product (the single-rank tests' bound)
+                from helpers import abs_tile, assert_tiles_equal, oracle_local
+                r1_ = cbg.block_range(A["m"], pr, grid.prow)[1]
+                c1_ = cbg.block_range(B["n"], pc, grid.pcol)[1]
+                if "bound" not in locals():
+                    bound = oracle_local(abs_tile(A), abs_tile(B))
+                    Cg = load_npz("largeseq_C_local_plus.npz")
+                try:
+                    assert_tiles_equal(C.tile.to_host(), cbg.sub_tile(Cg, r0, r1_, c0, c1_), rtol=1e-12,
+                                       bound=cbg.sub_tile(bound, r0, r1_, c0, c1_)["val"])
+                    mine_ok = b"1"
+                except AssertionError as e:
+                    print(rank, algo, ex, "per-entry", e, flush=True)
+                    mine_ok = b"0"
+                good = good and hc.allgather(0, mine_ok) == b"1" * world
             if rank == 0:
                 print(algo, ex, "OK" if good else f"BAD {tot} vs {gd}", flush=True)
             ok = ok and good

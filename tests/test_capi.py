@@ -63,3 +63,25 @@ def test_reference_adapter_compiles():
                        timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert os.path.exists(os.path.join(repo, "oracle", "_ref", "adapter_check"))
+
+
+def test_reference_multtiming_dropin_builds():
+    """The drop-in boundary: the reference's ReleaseTests/MultTiming.cpp,
+    compiled unmodified with integration/ParFriends_cbg.h force-included, resolves its
+    Mult_AnXBn_DoubleBuff / _Synch calls to the adapter's explicit specializations: the
+    binary imports libcbg's SUMMA and contains none of the reference's CPU SpGEMM
+    (LocalHybridSpGEMM, MultiwayMerge)."""
+    import shutil
+    import subprocess
+    if not os.path.isdir("/root/reference") or not os.path.exists("/opt/conda/lib/libmpi.so"):
+        pytest.skip("needs the reference sources and MPICH (build container only)")
+    if shutil.which("make") is None or shutil.which("nm") is None:
+        pytest.skip("no make / nm")
+    r = subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "adapter"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    exe = os.path.join(REPO, "oracle", "_ref", "multtiming_dropin")
+    und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True).stdout
+    assert "cbg_summa_spgemm" in und
+    syms = subprocess.run(["nm", "-C", exe], capture_output=True, text=True).stdout
+    assert "LocalHybridSpGEMM" not in syms and "MultiwayMerge" not in syms

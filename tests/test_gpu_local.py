@@ -344,49 +344,129 @@ print(json.dumps(dict(nnz=int(M.nnz), d=M.digest(), stats_nnz=st["nnz"], merge_i
     assert out[True]["merge_in"] > out[True]["nnz"] > 0
 
 
-def _tile_totals(cbg, scale, pr, pc, phases):
-    """nnz of every rank's C tile of a pr x pc grid, computed on this one GPU the way
-    the rank computes it (its A block row times its B block column, generated on
-    device as the (pr x 1) / (1 x pc) tiles), streamed in B-column phases; returns
-    (total nnz, total order violations)."""
+def _add(ds):
+    return dict(nnz=sum(d["nnz"] for d in ds), hs="%016x" % (sum(int(d["hs"], 16) for d in ds) % (1 << 64)),
+                hv="%016x" % (sum(int(d["hv"], 16) for d in ds) % (1 << 64)),
+                unsorted=sum(d["unsorted"] for d in ds))
+
+
+def _tile_digests(cbg, scale, pr, pc, phases=0):
+    """every rank's C tile of scale-`scale` A*A on a pr x pc grid, computed on this one
+    GPU the way the rank computes it (its A block row times its B block column,
+    generated on device as the (pr x 1) / (1 x pc) tiles), streamed in B-column
+    phases (0: picked from device memory, as the bench does); each phase digested at
+    its global offsets (row block start, column block start + phase offset), so the
+    sum is the digest of the whole C.  Returns (summed digest, phase plans)."""
+    from combblas_spmm_test_amd import block_range
     nv = 1 << scale
     grid = _self_grid_1x1(cbg)
-    tot = bad = 0
+    parts, plans = [], []
     for r in range(pr):
         Ar = cbg.rmat_tile(scale, 16, grid=(pr, 1), pos=(r, 0))
+        r0 = block_range(nv, pr, r)[0]
         for c in range(pc):
             Bc = cbg.rmat_tile(scale, 16, grid=(1, pc), pos=(0, c))
+            c0 = block_range(nv, pc, c)[0]
             A = cbg.SpParMat(Ar, grid, Ar.m, nv)
             B = cbg.SpParMat(Bc, grid, nv, Bc.n)
-            seen = []
-
-            def consume(ph, off, t):
-                d = t.digest(0, off)
-                seen.append((d["nnz"], d["unsorted"]))
-
-            cbg.MemEfficientSpGEMM(A, B, phases, on_phase=consume)
-            tot += sum(x[0] for x in seen)
-            bad += sum(x[1] for x in seen)
+            cbg.MemEfficientSpGEMM(A, B, phases, on_phase=lambda ph, off, t: parts.append(t.digest(r0, c0 + off)))
+            plans.append(cbg.phase_plan())
             Bc.free()
         Ar.free()
     grid.destroy()
-    return tot, bad
+    return _add(parts), plans
 
 
-def test_rank_tiles_scale22_2x2(cbg):
-    """Config 3's per-rank work on one GPU: the four C tiles of scale-22 A*A on a 2x2
-    grid (rank (r,c): A block row r times B block column c, 2 phases each); their
-    nonzeros add up to the reference's symbolic nnz(C) and every tile is row-sorted."""
-    tot, bad = _tile_totals(cbg, 22, 2, 2, 2)
-    assert tot == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"] and bad == 0
+def _oracle_large(key):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        return json.load(f)[key]
+
+
+@pytest.mark.parametrize("grid", [(2, 2), (4, 2)])
+def test_rank_tiles_scale22(cbg, grid):
+    """Config 3's per-rank work (2x2) and the bench's 8-GPU grid (4x2) on one GPU: every
+    rank's C tile of scale-22 A*A (its A block row times its B block column, phases
+    picked from memory), digested at its global offsets; the tiles' digests add up to
+    the oracle's digest of the whole C (tests/golden/oracle_large.json s22_ef16:
+    structure and values bit-exact), nnz to the reference's symbolic total."""
+    d, plans = _tile_digests(cbg, 22, grid[0], grid[1])
+    g = _oracle_large("s22_ef16")
+    assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (g["nnz"], g["hs"], g["hv"], 0)
+    assert d["nnz"] == G["rmat"]["s22_ef16"]["symbolic"]["nnzC"]
+    assert all(p["automatic"] and p["phases"] >= 1 for p in plans)
 
 
 def test_rank_tiles_scale24_2x4(cbg):
     """Config 4's per-rank work on one GPU: the eight C tiles of scale-24 A*A on a 2x4
-    grid (about 2.3e10 nonzeros = 275 GB per tile: streamed in 4 B-column phases);
-    their nonzeros add up to the reference's symbolic nnz(C) = 183,028,712,946."""
-    tot, bad = _tile_totals(cbg, 24, 2, 4, 4)
-    assert tot == G["rmat"]["s24_ef16"]["symbolic"]["nnzC"] and bad == 0
+    grid (about 2.3e10 nonzeros = 275 GB per tile: the phase count is picked from
+    device memory, C streamed per phase); their nonzeros add up to the reference's
+    symbolic nnz(C) = 183,028,712,946 and every tile is row-sorted."""
+    d, plans = _tile_digests(cbg, 24, 2, 4)
+    assert d["nnz"] == G["rmat"]["s24_ef16"]["symbolic"]["nnzC"] and d["unsorted"] == 0
+    assert all(p["automatic"] and p["phases"] >= 2 for p in plans)  # 275 GB of C per tile does not fit
+    g = _oracle_large("s24_ef16") if "s24_ef16" in _oracle_all() else None
+    if g is not None:
+        assert (d["nnz"], d["hs"], d["hv"]) == (g["nnz"], g["hs"], g["hv"])
+
+
+def _oracle_all():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        return json.load(f)
+
+
+def test_auto_phases_plan(cbg):
+    """MemEfficientSpGEMM's memory-driven phase count (ParFriends.h:482-535): the plan's
+    flops are the product's exact flops (from the tiles' count vectors); phases = 0 on
+    scale 18 (C = 5 GB) runs one phase; perProcessMemory = 2 GB forces several; the
+    streamed phases add up to the reference's digest either way."""
+    grid = _self_grid_1x1(cbg)
+    A = cbg.SpParMat.rmat(grid, 18)
+    B = cbg.SpParMat.rmat(grid, 18)
+    gd = G["rmat"]["s18_ef16"]["C_local_plus"]
+    for kw in ({}, {"perProcessMemory": 2}):
+        parts = []
+        cbg.MemEfficientSpGEMM(A, B, 0, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)), **kw)
+        plan, st = cbg.phase_plan(), cbg.last_stats()
+        d = _add(parts)
+        assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (gd["nnz"], gd["hs"], gd["hv"], 0), kw
+        assert plan["automatic"] and plan["flops"] == st["flops"] == G["rmat"]["s18_ef16"]["symbolic"]["flops"]
+        assert 0.8 * gd["nnz"] <= plan["nnz_est"] <= 1.3 * gd["nnz"], plan
+        if kw:
+            # 2 GB minus the inputs, half of it for C: 12 B x 4.3e8 entries needs several phases
+            assert plan["phases"] >= 4 and plan["c_budget_bytes"] < 1e9, plan
+        else:
+            assert plan["phases"] == 1, plan
+    A.tile.free()
+    B.tile.free()
+    grid.destroy()
+
+
+def test_phase_split_on_oom(cbg):
+    """A phase whose C does not fit (forced with the CBG_FAULT_C_BYTES test hook, read per
+    call) is computed as column halves of its B piece, each handed to the consumer at
+    its own offset: the digests still add up to the reference's."""
+    import os
+    grid = _self_grid_1x1(cbg)
+    A = cbg.SpParMat.rmat(grid, 14)
+    B = cbg.SpParMat.rmat(grid, 14)
+    gd = G["rmat"]["s14_ef16"]["C_local_plus"]
+    parts = []
+    os.environ["CBG_FAULT_C_BYTES"] = str(12 * gd["nnz"] // 5)
+    try:
+        cbg.MemEfficientSpGEMM(A, B, 2, on_phase=lambda ph, off, t: parts.append((ph, off, t.digest(0, off))))
+    finally:
+        del os.environ["CBG_FAULT_C_BYTES"]
+    plan = cbg.phase_plan()
+    d = _add([x[2] for x in parts])
+    assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (gd["nnz"], gd["hs"], gd["hv"], 0)
+    assert plan["oom_splits"] >= 2 and len(parts) >= 6 and sorted(set(x[0] for x in parts)) == [0, 1]
+    A.tile.free()
+    B.tile.free()
+    grid.destroy()
 
 
 @pytest.mark.parametrize("env", [{"CBG_BITMAP_BUDGET_GB": "0"}, {"CBG_BIG_FLOPS": "64"},
@@ -607,6 +687,63 @@ def test_galerkin_single_rank(cbg):
     g.destroy()
 
 
+@pytest.mark.parametrize("layout", ["1x1", "2x4"])
+def test_galerkin_scale22_vs_oracle(cbg, layout):
+    """Config 5 at its own size: GalerkinNew's S*(A*T) (GalerkinNew.cpp:96-110) for the
+    scale-22 R-MAT A (plus a diagonal) and the order-2 restriction T, plus-times within
+    1e-12 of the oracle entry by entry (all operands are positive, so |S||A||T| is the
+    oracle's product itself) and min-plus bit-exact.  1x1: one rank's PSpGEMMs.  2x4:
+    config 5's grid, every rank's two products computed on this GPU the way the PANEL
+    SUMMA does after its broadcasts (AT(:, c) = A T(:, c), then S(r, :) AT(:, c)), each
+    rank tile checked against its block of the oracle's product."""
+    from helpers import restriction_host, transpose_host
+    from combblas_spmm_test_amd import block_range, sub_tile
+    scale, n = 22, 1 << 22
+    dv = np.random.default_rng(7).uniform(0.5, 1.5, n)
+    g = _self_grid_1x1(cbg)
+    L = cbg.SpParMat.rmat(g, scale)
+    D = cbg.Tile.from_host(n, n, np.arange(n + 1, dtype=np.int64), np.arange(n, dtype=np.int32),
+                           np.arange(n, dtype=np.int32), dv)
+    Ad = cbg.MergeAll([L.tile, D])  # A = L + diag(dv) (L has no loops)
+    L.tile.free()
+    D.free()
+    Ah = Ad.to_host()
+    assert len(Ah["ir"]) == G["rmat"]["s22_ef16"]["A"]["nnz"] + n
+    Th = restriction_host(scale, 2)
+    Sh = transpose_host(Th)
+    for sr in ("plus", "minplus"):
+        ref = oracle_local(Sh, oracle_local(Ah, Th, sr=sr), sr=sr)
+        rtol = 1e-12 if sr == "plus" else 0.0
+        if layout == "1x1":
+            A = cbg.SpParMat(Ad, g, n, n)
+            T = cbg.SpParMat.restriction(g, scale, 2)
+            S = T.copy()
+            S.Transpose()
+            SAT = cbg.PSpGEMM(S, cbg.PSpGEMM(A, T, sr), sr)
+            assert_tiles_equal(SAT.tile.to_host(), ref, rtol=rtol, bound=ref["val"])
+            for X in (T, S, SAT):
+                X.tile.free()
+            continue
+        pr, pc = 2, 4
+        nc = n // 2
+        for c in range(pc):
+            c0, c1 = block_range(nc, pc, c)
+            Tc = cbg.Tile.from_dict(sub_tile(Th, 0, n, c0, c1))
+            ATc = cbg.LocalHybridSpGEMM(Ad, Tc, sr)
+            for r in range(pr):
+                r0, r1 = block_range(nc, pr, r)
+                Sr = cbg.Tile.from_dict(sub_tile(Sh, r0, r1, 0, n))
+                SATrc = cbg.LocalHybridSpGEMM(Sr, ATc, sr)
+                want = sub_tile(ref, r0, r1, c0, c1)
+                assert_tiles_equal(SATrc.to_host(), want, rtol=rtol, bound=want["val"])
+                for X in (Sr, SATrc):
+                    X.free()
+            Tc.free()
+            ATc.free()
+    Ad.free()
+    g.destroy()
+
+
 def test_galerkin_driver():
     """tools/galerkin.py end to end (one rank): splitting check passes, timings reported."""
     import json
@@ -779,10 +916,11 @@ def test_local_scale22_ef8_resident(cbg):
     assert d["nnz"] == sym["nnzC"] and st["flops"] == sym["flops"]
 
 
-@pytest.mark.parametrize("sr", ["plus", "minplus"])
-def test_phased_scale22_vs_oracle(cbg, sr):
-    """The bench's configuration: R-MAT scale-22 A*A as MemEfficientSpGEMM with 4
-    B-column phases on one GPU, each phase's C digested on the device as it is
+@pytest.mark.parametrize("sr,phases", [("plus", 0), ("plus", 3), ("plus", 4), ("minplus", 0)])
+def test_phased_scale22_vs_oracle(cbg, sr, phases):
+    """The bench's configuration: R-MAT scale-22 A*A as MemEfficientSpGEMM on one GPU with
+    the phase count picked from device memory (phases=0, what bench.py times: 3 phases),
+    and 3 and 4 phases forced; each phase's C digested on the device as it is
     streamed; the sum equals the oracle's digest of the whole C (24.8 G nonzeros,
     tests/golden/oracle_large.json; min-plus too) and nnz the reference's symbolic total."""
     import json
@@ -794,7 +932,11 @@ def test_phased_scale22_vs_oracle(cbg, sr):
     A = cbg.SpParMat(cbg.rmat_tile(22, 16), grid, nv, nv)
     B = cbg.SpParMat(cbg.rmat_tile(22, 16), grid, nv, nv)
     parts = []
-    cbg.MemEfficientSpGEMM(A, B, 4, sr=sr, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)))
+    cbg.MemEfficientSpGEMM(A, B, phases, sr=sr, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)))
+    plan = cbg.phase_plan()
+    assert plan["phases"] == (phases or plan["phases"]) and plan["automatic"] == (phases == 0)
+    if phases == 0:
+        assert 2 <= plan["phases"] <= 4 and plan["oom_splits"] == 0, plan
     hs = "%016x" % (sum(int(d["hs"], 16) for d in parts) % (1 << 64))
     hv = "%016x" % (sum(int(d["hv"], 16) for d in parts) % (1 << 64))
     nnz = sum(d["nnz"] for d in parts)
@@ -843,6 +985,27 @@ def test_reference_adapter_runs():
     mm = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sevenvertex.mtx")
     rc, out = _run_tool(("oracle", "_ref", "adapter_check"), [mm])
     assert rc == 0 and "ADAPTER OK" in out, out[-2000:]
+
+
+def test_reference_multtiming_unmodified_dropin():
+    """The drop-in: the reference's ReleaseTests/MultTiming.cpp compiled UNMODIFIED with
+    integration/ParFriends_cbg.h as one forced include (oracle/_ref/multtiming_dropin,
+    test infrastructure built against /root/reference).  Its
+    Mult_AnXBn_DoubleBuff<PlusTimesSRing<double,double>, double, SpDCCols<int,double>>
+    and Mult_AnXBn_Synch calls (MultTiming.cpp:58,71,83,92) run on MI355X through the
+    adapter's explicit specializations, on the reference's largeseq triples."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    os.environ["CBG_ADAPTER_VERBOSE"] = "1"
+    try:
+        rc, out = _run_tool(("oracle", "_ref", "multtiming_dropin"),
+                            [os.path.join(gold, "largeseq_input1_0.triples"), os.path.join(gold, "largeseq_input2_0.triples")])
+    finally:
+        del os.environ["CBG_ADAPTER_VERBOSE"]
+    assert rc == 0, out[-2000:]
+    assert "[cbg adapter] Mult_AnXBn_DoubleBuff on MI355X" in out and "[cbg adapter] Mult_AnXBn_Synch on MI355X" in out
+    assert "Double buffered multiplications finished" in out and "Synchronous multiplications finished" in out
+    assert "29677" in out  # C's nonzeros, printed by the reference's SpParHelper::Print / PrintInfo
 
 
 def test_tile_plugin_surface_python(cbg):

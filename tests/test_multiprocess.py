@@ -143,3 +143,36 @@ def test_rccl_multirank_gpu(grid, case):
     RCCL communicators, against the same golden digests as the host transport."""
     rc, out = launch(grid[0] * grid[1], ["rccl", str(grid[0]), str(grid[1]), case], timeout=300)
     assert rc == 0 and "MPOK" in out and "transport rccl" in out, out[:1500] + out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", [None, "2", "1/4"])
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2)])
+def test_narrow_uneven_pieces_gpu(grid, pipeline):
+    """B tiles 15 and 16 columns wide (31 x 31 on a 1 x 2 grid): every rank cuts the same
+    number of pipeline pieces (agreed from the narrowest tile), so PANEL never pairs
+    one rank's extra agree() with another's broadcast; products within 1e-12 of the
+    oracle for DoubleBuff/Synch, PANEL/STAGED and phases."""
+    env = {"CBG_PIPELINE": pipeline} if pipeline else {}
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "narrow"], timeout=300, env=env)
+    assert rc == 0 and "MPOK" in out, out[:1500] + out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("grid", [(1, 2), (2, 2)])
+def test_layout_mismatch_gpu(grid):
+    """A tile off the block layout (one rank's A tile a column short): STAGED's stage
+    slices and PANEL's gathered widths both return CBG_ERR_DIMMISMATCH on every rank
+    (reference: MPI_Abort(DIMMISMATCH)); the grid multiplies correctly afterwards."""
+    rc, out = launch(grid[0] * grid[1], ["gpu", str(grid[0]), str(grid[1]), "mismatch"], timeout=300)
+    assert rc == 0 and "MPOK" in out, out[:1500] + out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gpu", "rccl"])
+def test_redist_fault_gpu(mode):
+    """Transpose and BlockSplit under the collective error protocol: a receive-buffer
+    allocation that fails on one rank (CBG_FAULT_INJECT_REDIST) is returned by every
+    rank of a 2x2 grid, over the host transport and over RCCL; both then work."""
+    rc, out = launch(4, [mode, "2", "2", "redist_fault"], timeout=300)
+    assert rc == 0 and "MPOK" in out, out[:1500] + out[-3000:]
