@@ -362,9 +362,11 @@ def main():
                                 "flops_rank0": plans[-1]["flops"], "nnz_est_rank0": plans[-1]["nnz_est"],
                                 "c_budget_gb_rank0": round(plans[-1]["c_budget_bytes"] / 1e9, 1),
                                 "oom_splits": plans[-1]["oom_splits"],
+                                "plan_ms_per_step": [round(p_["plan_ms"], 2) for p_ in plans[-a.steps:]],
                                 "rule": "MemEfficientSpGEMM(phases=0): flops of the rank's product from tile count "
-                                        "vectors x the compression of an exact symbolic of every 64th B column, "
-                                        "12 B per entry against half of the free HBM, inside each timed step"}
+                                        "vectors (x the compression of an exact symbolic of a sample when the flops "
+                                        "bound asks for > 1 phase), 12 B per entry against half of the free HBM, "
+                                        "inside each timed step"}
                                if plans else None),
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
                                      "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],

@@ -130,7 +130,8 @@ def lib():
         "cbg_summa_spgemm_phased": ([vp, T, T, i64, i64, i32, i32, i32, i32, PHASE_FN, vp, T], i32),
         "cbg_summa_spgemm_memeff": ([vp, T, T, i64, i64, i32, i32, i32, i32, i64, PHASE_FN, vp, T], i32),
         "cbg_last_phase_plan": ([ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(i64),
-                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)], i32),
+                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double)],
+                                i32),
         "cbg_tile_transpose": ([T, T], i32),
         "cbg_tile_dim_apply": ([T, i32, ctypes.POINTER(ctypes.c_double), i32], i32),
         "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
@@ -394,10 +395,11 @@ def phase_plan():
     rank's product flops and nnz(C) estimate, the C bytes a phase was allowed, and
     phases split in column halves after an out-of-memory."""
     a, b, c, d, e, f = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int()
+    g = ctypes.c_double()
     lib().cbg_last_phase_plan(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d), ctypes.byref(e),
-                              ctypes.byref(f))
+                              ctypes.byref(f), ctypes.byref(g))
     return dict(phases=a.value, automatic=bool(b.value), flops=c.value, nnz_est=d.value, c_budget_bytes=e.value,
-                oom_splits=f.value)
+                oom_splits=f.value, plan_ms=g.value)
 
 
 def merge_stats():

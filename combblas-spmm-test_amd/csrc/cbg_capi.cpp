@@ -488,7 +488,7 @@ int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A, const cbg_tile* B, i
 }
 
 int cbg_last_phase_plan(int* phases, int* automatic, int64_t* flops, int64_t* nnz_est, double* c_budget_bytes,
-                        int* oom_splits) {
+                        int* oom_splits, double* plan_ms) {
   const cbg::PhasePlan& p = cbg::phase_plan();
   if (phases) *phases = p.phases;
   if (automatic) *automatic = p.automatic;
@@ -496,6 +496,7 @@ int cbg_last_phase_plan(int* phases, int* automatic, int64_t* flops, int64_t* nn
   if (nnz_est) *nnz_est = p.nnz_est;
   if (c_budget_bytes) *c_budget_bytes = p.c_budget_bytes;
   if (oom_splits) *oom_splits = cbg::summa_info().oom_splits;
+  if (plan_ms) *plan_ms = p.ms;
   return CBG_OK;
 }
 

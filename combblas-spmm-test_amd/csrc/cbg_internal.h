@@ -147,6 +147,13 @@ struct LocalStats {
 void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& C, hipStream_t s,
                   LocalStats* st = nullptr, OutSink* sink = nullptr);
 LocalStats& thread_stats();
+// CUs the persistent slab kernels leave free for communication (cbg_local.hip)
+int& comm_reserve_cus();
+struct CommReserve {  // scope of a local multiply that runs while a broadcast is in flight
+  int prev;
+  explicit CommReserve(int cus) : prev(comm_reserve_cus()) { comm_reserve_cus() = cus; }
+  ~CommReserve() { comm_reserve_cus() = prev; }
+};
 // merges run as products (cbg_merge.hip) but are not SpGEMM work: their
 // multiplies are kept out of thread_stats() and summed here instead
 struct MergeStats {
@@ -168,6 +175,7 @@ struct PhasePlan {
   int phases = 0, automatic = 0;
   int64_t flops = 0, nnz_est = 0;
   double c_budget_bytes = 0;
+  double ms = 0;  // host time of the planning (collectives and sample included)
 };
 PhasePlan& phase_plan();
 SummaInfo& summa_info();
@@ -232,11 +240,15 @@ bool tile_equal(const cbg_tile& a, const cbg_tile& b, double eps, hipStream_t s)
 // phase planning: dim 0 = nonzeros per column (length n), 1 = per row (length m),
 // into the device array d zero-padded to `padded` entries (stream synchronized)
 void tile_counts_device(const cbg_tile& t, int dim, int32_t* d, int64_t padded, hipStream_t s);
+// sum over B's entries (k, j) of a[k] (device array of B.m values): A*B's flops for A's column counts
+int64_t entry_sum_device(const cbg_tile& B, const int32_t* a, hipStream_t s);
 // sum_k a[k] * b[k] over k < K with a, b stored as blocks (see cbg_tile.hip)
 int64_t blocked_dot_device(const int32_t* a, int64_t astride, const std::vector<int64_t>& aoff, const int32_t* b,
                            int64_t bstride, const std::vector<int64_t>& boff, int64_t K, hipStream_t s);
-// every stride-th nonempty column of T (same shape and column ids)
+// the columns of T whose id is a multiple of stride (same shape and ids), and
+// the rows whose id is (renumbered row / stride: ceil(m / stride) rows)
 void tile_sample_cols(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s);
+void tile_sample_rows(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s);
 // estimateFLOP + estimateNNZ_Hash totals of A*B without the numeric phase
 void local_symbolic(const cbg_tile& A, const cbg_tile& B, hipStream_t s, int64_t* flops, int64_t* nnz);
 

@@ -36,6 +36,8 @@ __constant__ int c_dbg;
 //   16: k_num_slab accumulates per-phase wall time (thread 0 of every block) into g_phase
 __device__ unsigned long long g_phase[16];
 //   32: k_num_slab counts into g_stat: slabs, non-full slabs, B entries, B entries of non-full slabs, products, nout
+//   64: k_sym_panel skips the hash-count products of sparse pairs and panel groups
+//  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
 __device__ unsigned long long g_stat[8];
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
   if ((c_dbg & 16) && threadIdx.x == 0) {
@@ -519,6 +521,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
       __syncthreads();
       int count = 0;
+      if (!(c_dbg & 64))
       block_products<BS>(
           pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
           [&](const SegI& g, int u) { return irA[g.off + u]; },
@@ -609,7 +612,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
         const int j = f * FW + q + lane;
         if (j < words) {
           const unsigned x = bm[j];
-          if (gdst) st_stream(&gdst[j], x);
+          if (gdst && !(c_dbg & 128)) st_stream(&gdst[j], x);
           c += __popc(x);
         }
       }
@@ -706,6 +709,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   const int32_t* __restrict__ irA = a.irA;
   const int* pref = L.pref;
   const int* st = L.st;
+  if (!(c_dbg & 64))
   block_products<BS>(
       pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
       [&](const SegI& g, int u) { return irA[g.off + u]; },
@@ -1584,6 +1588,17 @@ static int device_cus() {
   return cus;
 }
 
+// CUs the persistent kernels (slab queues) may fill: all of them, less
+// comm_reserve_cus() while a broadcast of the SUMMA is in flight on the comm
+// stream.  A persistent block never retires before its queue drains, so a grid
+// of one block per CU would keep RCCL's broadcast kernels off the GPU until the
+// kernel ends; the reserved CUs let them run beside it.
+int& comm_reserve_cus() {
+  static thread_local int r = 0;
+  return r;
+}
+static int active_cus() { return std::max(1, device_cus() - comm_reserve_cus()); }
+
 template <class K>
 static void set_lds(K kernel, size_t bytes) {
   if (bytes > 65536) CBG_HIP(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
@@ -1685,7 +1700,7 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   }
   int lm = 0;
   while ((1LL << lm) < A.m) ++lm;  // emit buckets span [0, 2^lm)
-  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
@@ -1720,7 +1735,7 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
       CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
       if (per_cu < 1) per_cu = 1;
     }
-    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                        A.n + 1, A.ir, valA, C.ir, C.val);
   };
@@ -1743,7 +1758,7 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
       CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
       if (per_cu < 1) per_cu = 1;
     }
-    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * device_cus());
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                        A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p);
   };

@@ -269,6 +269,10 @@ static void allgather_device(cbg_grid* g, int which, const void* in, void* out, 
   check_usable(g);
   if (bytes == 0) return;
   const int P = comm_size(g, which);
+  if (P == 1) {
+    CBG_HIP(hipMemcpy(out, in, bytes, hipMemcpyDeviceToDevice));
+    return;
+  }
   if (g->host_mode) {
     std::vector<char> h(bytes), all((size_t)P * bytes);
     CBG_HIP(hipMemcpy(h.data(), in, bytes, hipMemcpyDeviceToHost));
@@ -526,6 +530,11 @@ static void multiply_to_fn(const cbg_tile& A, const cbg_tile& B, int sr, hipStre
   if (r && !cb_rc) cb_rc = r;
 }
 
+static int comm_reserve_default() {
+  static const char* e = getenv("CBG_COMM_RESERVE_CUS");
+  return e ? std::max(0, atoi(e)) : 8;
+}
+
 static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                        const std::vector<int64_t>& cuts_in, cbg_phase_fn fn, void* user, cbg_tile* C,
                        bool adaptive = false) {
@@ -680,6 +689,9 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     if (local) continue;  // agreed at the next step
     local = step([&] {
       maybe_inject_fault(g);
+      // piece p+1's broadcast runs on the comm stream during this multiply:
+      // the persistent kernels leave CBG_COMM_RESERVE_CUS (8) CUs to it
+      CommReserve reserve(p + 1 < np && !g->host_mode ? comm_reserve_default() : 0);
       if (p == 0 && pc > 1) {
         std::vector<cbg_tile> parts(pc);
         for (int s = 0; s < pc; ++s) parts[s] = s == g->pcol ? A : Ar[s].t;
@@ -843,6 +855,7 @@ static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
     if (local) continue;
     local = step([&] {
       maybe_inject_fault(g);
+      CommReserve reserve(s + 1 < S && !g->host_mode ? comm_reserve_default() : 0);
       const cbg_tile& a = st[s].sa == g->pcol ? myA[s].t : Ar[s].t;
       const cbg_tile& b = st[s].sb == g->prow ? myB[s].t : Bc[s].t;
       TileGuard P;
@@ -929,9 +942,12 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 //    of nnz(A(:,k) in my grid row) * nnz(B(k,:) in my grid column), from the
 //    column counts of A's tiles (allgathered along the grid row) and the row
 //    counts of B's tiles (along the grid column): count vectors, not tiles;
-//  * nnz(C) <= flops; on one rank the compression nnz/flops is measured by an
-//    exact symbolic of every 64th nonempty column of B (~1/64 of a symbolic
-//    pass) and the estimate is flops x ratio x 1.1;
+//  * nnz(C) <= flops; the compression nnz/flops is measured by an exact
+//    symbolic of a sample of the product (one rank: every 128th column of B, ~1/128
+//    of a symbolic pass; a grid: every 8th row of the A block row times every
+//    16th column of the B block column, gathered like the SUMMA's tiles) and the
+//    estimate is flops x ratio x 1.1 -- only where the flops bound alone asks for
+//    more than one phase on some rank;
 //  * the C bytes a phase may take: CBG_PHASE_MEM_FRAC (0.5) of the memory left
 //    after the tiles the SUMMA gathers -- perProcessMemory (GB, like the
 //    reference) when given, else the device's free memory plus libcbg's pool
@@ -955,6 +971,13 @@ static double phase_mem_frac() {
 static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t K, int64_t mem_gb, int64_t n_min,
                        int fallback, int& phases) {
   hipStream_t cs = g->compute;
+  static const bool dbg = getenv("CBG_DEBUG_PLAN") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (dbg)
+      std::fprintf(stderr, "[cbg plan] %s at %.2f ms\n", what,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+  };
   const int pr = g->pr, pc = g->pc;
   // widths of A's tiles along my grid row and heights of B's along my grid column
   std::vector<int64_t> WA(pc), HB(pr);
@@ -965,36 +988,39 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   for (auto h : HB) hmax = std::max(hmax, h), sb += h;
   int rc = agree(g, (sa != K || sb != K) ? CBG_ERR_DIMMISMATCH : CBG_OK);
   if (rc) return rc;
-  // the count vectors, padded to the widest tile, gathered on the device
-  DBuf<int32_t> ca(std::max<int64_t>(wmax, 1)), rb(std::max<int64_t>(hmax, 1));
-  DBuf<int32_t> CA(std::max<int64_t>(wmax * pc, 1)), RB(std::max<int64_t>(hmax * pr, 1));
-  rc = agree(g, step([&] { tile_counts_device(A, 0, ca.p, wmax, cs), tile_counts_device(B, 1, rb.p, hmax, cs); }));
-  if (rc) return rc;
-  allgather_device(g, COMM_ROW, ca.p, CA.p, sizeof(int32_t) * wmax);
-  allgather_device(g, COMM_COL, rb.p, RB.p, sizeof(int32_t) * hmax);
   int64_t flops = 0;
-  rc = agree(g, step([&] {
-    std::vector<int64_t> aoff(pc + 1, 0), boff(pr + 1, 0);
-    for (int s = 0; s < pc; ++s) aoff[s + 1] = aoff[s] + WA[s];
-    for (int s = 0; s < pr; ++s) boff[s + 1] = boff[s] + HB[s];
-    flops = blocked_dot_device(CA.p, wmax, aoff, RB.p, hmax, boff, K, cs);
-  }));
-  if (rc) return rc;
-  // compression ratio from a column sample (one rank: no broadcast needed)
-  double ratio = 1.0;
-  if (g->nranks == 1 && flops > 0) {
-    static const char* es = getenv("CBG_PHASE_SAMPLE");
-    const int stride = es ? std::max(1, atoi(es)) : 64;
-    rc = step([&] {
-      TileGuard Bs;
-      tile_sample_cols(B, stride, Bs.t, cs);
-      int64_t f = 0, z = 0;
-      local_symbolic(A, Bs.t, cs, &f, &z);
-      if (f > 0) ratio = std::min(1.0, 1.1 * (double)z / (double)f);
-    });
-    if ((rc = agree(g, rc))) return rc;
+  if (g->nranks == 1) {
+    // one rank: the flops straight from A's column counts and B's entries
+    DBuf<int32_t> ca(std::max<int64_t>(A.n, 1));
+    rc = agree(g, step([&] {
+      tile_counts_device(A, 0, ca.p, A.n, cs);
+      flops = entry_sum_device(B, ca.p, cs);
+    }));
+  } else {
+    // the count vectors, padded to the widest tile, gathered on the device
+    DBuf<int32_t> ca(std::max<int64_t>(wmax, 1)), rb(std::max<int64_t>(hmax, 1));
+    DBuf<int32_t> CA(std::max<int64_t>(wmax * pc, 1)), RB(std::max<int64_t>(hmax * pr, 1));
+    rc = agree(g, step([&] { tile_counts_device(A, 0, ca.p, wmax, cs), tile_counts_device(B, 1, rb.p, hmax, cs); }));
+    if (rc) return rc;
+    mark("counts");
+    allgather_device(g, COMM_ROW, ca.p, CA.p, sizeof(int32_t) * wmax);
+    allgather_device(g, COMM_COL, rb.p, RB.p, sizeof(int32_t) * hmax);
+    mark("count allgathers");
+    rc = agree(g, step([&] {
+      std::vector<int64_t> aoff(pc + 1, 0), boff(pr + 1, 0);
+      for (int s = 0; s < pc; ++s) aoff[s + 1] = aoff[s] + WA[s];
+      for (int s = 0; s < pr; ++s) boff[s + 1] = boff[s] + HB[s];
+      flops = blocked_dot_device(CA.p, wmax, aoff, RB.p, hmax, boff, K, cs);
+    }));
   }
-  // memory left for C after the tiles the SUMMA gathers (mine are already held)
+  if (rc) return rc;
+  mark("flops");
+  // compression nnz/flops of a sample of this rank's product: one rank: every
+  // 64th column of B (CBG_PHASE_SAMPLE); a grid: every 8th row of the A block row
+  // times every 16th column of the B block column, the samples broadcast like
+  // the SUMMA's tiles (1/8 and 1/16 of their bytes); ids, not positions, so the
+  // tiles of a grid row / column sample the same rows / columns
+  // (skipped, agreed, where the flops bound alone leaves one phase on every rank)
   auto tbytes = [](const cbg_tile& t) { return (double)(8 * (t.nzc + 1) + 4 * t.nzc + 12 * t.nnz); };
   const double gathered = (pc - 1) * tbytes(A) + (pr - 1) * tbytes(B);
   double avail;
@@ -1006,6 +1032,74 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     avail = (double)fr + (double)pool().bytes_cached() - gathered;
   }
   const double budget = phase_mem_frac() * avail;
+  int64_t need_sample = 0;
+  if ((rc = agree_val(g, CBG_OK, flops > 0 && 12.0 * (double)flops > budget ? 1 : 0, nullptr, &need_sample)))
+    return rc;
+  double ratio = 1.0;
+  if (need_sample) {
+    static const char* es = getenv("CBG_PHASE_SAMPLE");
+    const int cstride = es ? std::max(1, atoi(es)) : (g->nranks == 1 ? 128 : 16);
+    const int rstride = g->nranks == 1 ? 1 : 8;
+    TileGuard As, Bs;
+    rc = agree(g, step([&] {
+      if (rstride > 1) tile_sample_rows(A, rstride, As.t, cs);
+      tile_sample_cols(B, cstride, Bs.t, cs);
+    }));
+    if (rc) return rc;
+    const cbg_tile& Amine = rstride > 1 ? As.t : A;
+    int64_t ea[4], eb[4];
+    tile_ess(Amine, ea);
+    tile_ess(Bs.t, eb);
+    std::vector<int64_t> EA((size_t)4 * pc), EB((size_t)4 * pr);
+    allgather_i64(g, COMM_ROW, ea, EA.data(), 4);
+    allgather_i64(g, COMM_COL, eb, EB.data(), 4);
+    std::vector<TileGuard> Ar(pc), Bc(pr);
+    rc = agree(g, step([&] {
+      for (int q = 0; q < pc; ++q)
+        if (q != g->pcol) alloc_like(Ar[q].t, &EA[4 * q]);
+      for (int q = 0; q < pr; ++q)
+        if (q != g->prow) alloc_like(Bc[q].t, &EB[4 * q]);
+    }));
+    if (rc) return rc;
+    int64_t fs = 0, zs = 0;
+    rc = agree(g, step([&] {
+      bcast_group(g, [&] {
+        for (int q = 0; q < pc; ++q)
+          bcast_tile(g, COMM_ROW, q, &EA[4 * q], q == g->pcol ? const_cast<cbg_tile&>(Amine) : Ar[q].t, q == g->pcol);
+      });
+      bcast_group(g, [&] {
+        for (int q = 0; q < pr; ++q) bcast_tile(g, COMM_COL, q, &EB[4 * q], q == g->prow ? Bs.t : Bc[q].t, q == g->prow);
+      });
+      wait_comm(g);
+      TileGuard Ap, Bp;
+      const cbg_tile* Au = &Amine;
+      const cbg_tile* Bu = &Bs.t;
+      if (pc > 1) {
+        std::vector<cbg_tile> parts(pc);
+        std::vector<int64_t> off(pc, 0);
+        for (int q = 0; q < pc; ++q) {
+          parts[q] = q == g->pcol ? Amine : Ar[q].t;
+          if (q) off[q] = off[q - 1] + WA[q - 1];
+        }
+        tile_concat_cols(parts, off, Amine.m, K, Ap.t, cs);
+        Au = &Ap.t;
+      }
+      if (pr > 1) {
+        std::vector<cbg_tile> parts(pr);
+        std::vector<int64_t> off(pr, 0);
+        for (int q = 0; q < pr; ++q) {
+          parts[q] = q == g->prow ? Bs.t : Bc[q].t;
+          if (q) off[q] = off[q - 1] + HB[q - 1];
+        }
+        tile_concat_rows(parts, off, K, B.n, Bp.t, cs);
+        Bu = &Bp.t;
+      }
+      local_symbolic(*Au, *Bu, cs, &fs, &zs);
+    }));
+    if (rc) return rc;
+    if (fs > 0) ratio = std::min(1.0, 1.1 * (double)zs / (double)fs);
+    mark("sample symbolic");
+  }
   const double need = 12.0 * ratio * (double)flops;
   int64_t want = budget > 0 ? (int64_t)std::ceil(need / budget) : fallback;  // the reference keeps the given phases
   want = std::max<int64_t>(1, std::min<int64_t>(want, std::max<int64_t>(1, n_min)));
@@ -1017,6 +1111,8 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   pp.flops = flops;
   pp.nnz_est = (int64_t)(ratio * (double)flops);
   pp.c_budget_bytes = budget;
+  pp.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  mark("planned");
   return CBG_OK;
 }
 
@@ -1037,6 +1133,9 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
   check_usable(g);
   arm_fault(g);
   phase_plan() = PhasePlan{};
+  // every local multiply of this call (the plan's sample included on one rank)
+  // multiplies the same A: its column maps are built once
+  APrepScope aprep_scope;
   const bool automatic = phases <= 0 || mem_gb > 0;
   if (!automatic && phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
   int rc = A_gncol != B_gnrow ? CBG_ERR_DIMMISMATCH : CBG_OK;

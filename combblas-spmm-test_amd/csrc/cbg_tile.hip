@@ -879,6 +879,28 @@ __global__ void k_blocked_dot(const int32_t* __restrict__ a, int64_t astride, co
   acc = (unsigned long long)wave_sum64((long long)acc);
   if (lane_id() == 0 && acc) atomicAdd(out, acc);
 }
+// sum over the entries (k, j) of B of a[k]: the flops of A*B when a holds A's
+// column counts (estimateFLOP's total without row counts of B)
+__global__ void k_entry_sum(int64_t nnz, const int32_t* __restrict__ ir, const int32_t* __restrict__ a,
+                            unsigned long long* __restrict__ out) {
+  unsigned long long acc = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x)
+    acc += (unsigned)a[ir[i]];
+  acc = (unsigned long long)wave_sum64((long long)acc);
+  if (lane_id() == 0 && acc) atomicAdd(out, acc);
+}
+int64_t entry_sum_device(const cbg_tile& B, const int32_t* a, hipStream_t s) {
+  DBuf<unsigned long long> d(1);
+  CBG_HIP(hipMemsetAsync(d.p, 0, sizeof(unsigned long long), s));
+  if (B.nnz > 0)
+    hipLaunchKernelGGL(k_entry_sum, dim3((unsigned)std::min<int64_t>((B.nnz + 255) / 256, 4096)), dim3(256), 0, s,
+                       B.nnz, B.ir, a, d.p);
+  unsigned long long h = 0;
+  CBG_HIP(hipMemcpyAsync(&h, d.p, sizeof(h), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipStreamSynchronize(s));
+  return (int64_t)h;
+}
+
 int64_t blocked_dot_device(const int32_t* a, int64_t astride, const std::vector<int64_t>& aoff, const int32_t* b,
                            int64_t bstride, const std::vector<int64_t>& boff, int64_t K, hipStream_t s) {
   DotSegs sg{};
@@ -898,42 +920,87 @@ int64_t blocked_dot_device(const int32_t* a, int64_t astride, const std::vector<
   return (int64_t)h;
 }
 
-// every stride-th nonempty column (DCSC positions 0, stride, 2 stride, ...) of T,
-// same shape and column ids: a wave per sampled column copies its entries
-__global__ void k_sample_len(int64_t ns, int stride, const int64_t* __restrict__ cp, int64_t* __restrict__ len) {
+// Samples of a tile for the compression estimate: the columns whose id is a
+// multiple of `stride` (every tile of a grid column keeps the same columns), or
+// the rows whose id is a multiple of `stride`, renumbered row / stride (every
+// tile of a grid row keeps the same rows).  Ids, not positions: R-MAT's ids are
+// scrambled, so either is a uniform sample.
+__global__ void k_sample_col_len(int64_t nzc, int stride, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
+                                 int64_t* __restrict__ len, int64_t* __restrict__ flag) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < ns) len[i] = cp[i * stride + 1] - cp[i * stride];
+  if (i >= nzc) return;
+  const bool keep = jc[i] % stride == 0;
+  len[i] = keep ? cp[i + 1] - cp[i] : 0;
+  flag[i] = keep;
 }
-__global__ void k_sample_copy(int64_t ns, int stride, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
-                              const int32_t* __restrict__ ir, const double* __restrict__ val,
-                              const int64_t* __restrict__ ocp, int32_t* __restrict__ ojc, int32_t* __restrict__ oir,
+__global__ void k_sample_row_len(int64_t nzc, int stride, const int64_t* __restrict__ cp,
+                                 const int32_t* __restrict__ ir, int64_t* __restrict__ len, int64_t* __restrict__ flag) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  if (i >= nzc) return;
+  int c = 0;
+  for (int64_t q = cp[i] + lane_id(); q < cp[i + 1]; q += WAVE) c += ir[q] % stride == 0;
+  c = wave_sum(c);
+  if (lane_id() == 0) {
+    len[i] = c;
+    flag[i] = c > 0;
+  }
+}
+// a wave per kept column; rows == true: keep only rows % stride == 0, renumbered
+__global__ void k_sample_copy(int64_t nzc, int stride, bool rows, const int64_t* __restrict__ cp,
+                              const int32_t* __restrict__ jc, const int32_t* __restrict__ ir,
+                              const double* __restrict__ val, const int64_t* __restrict__ len,
+                              const int64_t* __restrict__ off, const int64_t* __restrict__ col,
+                              int64_t* __restrict__ ocp, int32_t* __restrict__ ojc, int32_t* __restrict__ oir,
                               double* __restrict__ oval) {
   const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
-  if (i >= ns) return;
-  const int64_t src = cp[i * stride], n = cp[i * stride + 1] - src, dst = ocp[i];
-  if (lane_id() == 0) ojc[i] = jc[i * stride];
-  for (int64_t q = lane_id(); q < n; q += WAVE) {
-    oir[dst + q] = ir[src + q];
-    oval[dst + q] = val[src + q];
+  if (i >= nzc || len[i] == 0) return;
+  const int lane = lane_id();
+  if (lane == 0) {
+    ojc[col[i]] = jc[i];
+    ocp[col[i]] = off[i];
+  }
+  int64_t dst = off[i];
+  for (int64_t q0 = cp[i]; q0 < cp[i + 1]; q0 += WAVE) {
+    const int64_t q = q0 + lane;
+    const bool in = q < cp[i + 1];
+    const int r = in ? ir[q] : 0;
+    const bool keep = in && (!rows || r % stride == 0);
+    const unsigned long long m = __ballot(keep);
+    if (keep) {
+      const int64_t at = dst + __popcll(m & ((1ull << lane) - 1ull));
+      oir[at] = rows ? r / stride : r;
+      oval[at] = val[q];
+    }
+    dst += __popcll(m);
   }
 }
-void tile_sample_cols(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s) {
-  const int64_t ns = T.nzc > 0 ? (T.nzc + stride - 1) / stride : 0;
-  if (ns == 0) {
-    tile_alloc_device(out, T.m, T.n, 0, 0);
+static void tile_sample(const cbg_tile& T, int stride, bool rows, cbg_tile& out, hipStream_t s) {
+  const int64_t m = rows ? (T.m + stride - 1) / stride : T.m;
+  const int64_t nz = T.nzc;
+  if (nz == 0) {
+    tile_alloc_device(out, m, T.n, 0, 0);
     return;
   }
-  DBuf<int64_t> len(ns + 1), off(ns + 1);
-  hipLaunchKernelGGL(k_sample_len, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, s, ns, stride, T.cp, len.p);
-  exclusive_scan_i64(len.p, off.p, ns, s);
-  int64_t nnz = 0;
-  CBG_HIP(hipMemcpyAsync(&nnz, off.p + ns, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  DBuf<int64_t> len(nz + 1), flag(nz + 1), off(nz + 1), col(nz + 1);
+  if (rows)
+    hipLaunchKernelGGL(k_sample_row_len, dim3((unsigned)((nz * WAVE + 255) / 256)), dim3(256), 0, s, nz, stride, T.cp,
+                       T.ir, len.p, flag.p);
+  else
+    hipLaunchKernelGGL(k_sample_col_len, dim3((unsigned)((nz + 255) / 256)), dim3(256), 0, s, nz, stride, T.cp, T.jc,
+                       len.p, flag.p);
+  exclusive_scan_i64(len.p, off.p, nz, s);
+  exclusive_scan_i64(flag.p, col.p, nz, s);
+  int64_t h[2];
+  CBG_HIP(hipMemcpyAsync(&h[0], off.p + nz, 8, hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&h[1], col.p + nz, 8, hipMemcpyDeviceToHost, s));
   CBG_HIP(hipStreamSynchronize(s));
-  tile_alloc_device(out, T.m, T.n, nnz, ns);
-  CBG_HIP(hipMemcpyAsync(out.cp, off.p, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToDevice, s));
-  hipLaunchKernelGGL(k_sample_copy, dim3((unsigned)((ns * WAVE + 255) / 256)), dim3(256), 0, s, ns, stride, T.cp, T.jc,
-                     T.ir, T.val, off.p, out.jc, out.ir, out.val);
+  tile_alloc_device(out, m, T.n, h[0], h[1]);
+  hipLaunchKernelGGL(k_sample_copy, dim3((unsigned)((nz * WAVE + 255) / 256)), dim3(256), 0, s, nz, stride, rows, T.cp,
+                     T.jc, T.ir, T.val, len.p, off.p, col.p, out.cp, out.jc, out.ir, out.val);
+  CBG_HIP(hipMemcpyAsync(out.cp + h[1], &h[0], 8, hipMemcpyHostToDevice, s));
   CBG_HIP(hipStreamSynchronize(s));
 }
+void tile_sample_cols(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s) { tile_sample(T, stride, false, out, s); }
+void tile_sample_rows(const cbg_tile& T, int stride, cbg_tile& out, hipStream_t s) { tile_sample(T, stride, true, out, s); }
 
 }  // namespace cbg

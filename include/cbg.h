@@ -243,9 +243,10 @@ int cbg_summa_spgemm_memeff(cbg_grid* g, const cbg_tile* A_local, const cbg_tile
                             int64_t per_process_memory_gb, cbg_phase_fn fn, void* user, cbg_tile* C_local);
 /* the last (memeff / phased) call's phase plan: phases run, whether they were
  * chosen from memory, this rank's product flops and estimated nnz(C), the C bytes
- * a phase was allowed, and phases split in halves after an out-of-memory */
+ * a phase was allowed, phases split in halves after an out-of-memory, and the
+ * host ms the planning took */
 int cbg_last_phase_plan(int* phases, int* automatic, int64_t* flops, int64_t* nnz_est, double* c_budget_bytes,
-                        int* oom_splits);
+                        int* oom_splits, double* plan_ms);
 
 /* SpParMat::Transpose (SpParMat.cpp:3528-3590), collective over a square grid:
  * out = this rank's tile of the transposed matrix (the transpose of the
