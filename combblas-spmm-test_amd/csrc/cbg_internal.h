@@ -46,6 +46,7 @@ class DevicePool {
   void* alloc(size_t bytes);
   void free(void* p);
   void trim();  // release every cached block
+  bool release_largest_cached();  // hipFree the largest cached (non-growable) block; false if none
   void* reserve_growable(size_t max_bytes);
   void grow(void* base, size_t bytes);  // map [base, base + bytes)
   size_t bytes_in_use() const { return in_use_; }

@@ -38,6 +38,7 @@ __device__ unsigned long long g_phase[16];
 //   32: k_num_slab counts into g_stat: slabs, non-full slabs, B entries, B entries of non-full slabs, products, nout
 //   64: k_sym_panel skips the hash-count products of sparse pairs and panel groups
 //  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
+//  256: k_sym_panel leaves a hash-mode pair or panel group right after its staging
 __device__ unsigned long long g_stat[8];
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
   if ((c_dbg & 16) && threadIdx.x == 0) {
@@ -125,7 +126,7 @@ __global__ void k_colmap_panel1(int64_t nA1, const int2* __restrict__ cmap, int2
   }
 }
 
-constexpr int MAXBINS = 12;
+constexpr int MAXBINS = 16;
 struct BinThr {
   int64_t t[MAXBINS];  // bin b <=> key <= t[b] (first match); last bin catches the rest
   int nb;
@@ -407,7 +408,7 @@ __global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cp
 // flops -- and a group whose nonzeros fit one hash slab becomes ONE sparse
 // slab over the group's rows.  That shares the B column staging and column
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
-constexpr int GROUP_LOG_MAX = 4;      // groups of up to 16 panels
+constexpr int GROUP_LOG_MAX = 6;      // groups of up to 64 panels (scale 24: R = 64 panels per column)
 constexpr int GROUP_PRODUCTS = 3072;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
 #ifndef CBG_SYM_WAVES_OF_UNITS  // persistent symbolic grid: resident blocks x this
 #define CBG_SYM_WAVES_OF_UNITS 32  // 1: -2 % (static stride meets hub-column imbalance); 16-32: +1 % at scale 22
@@ -517,6 +518,15 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     int T = 512;
     while (T < 2 * total) T <<= 1;
     if (total <= SPARSE_SLAB_MAX && T <= pwords) {
+      if (c_dbg & 256) {
+        __syncthreads();
+        if (tid == 0) {
+          nslab[br] = 0;
+          cnt_br[br] = 0;
+          if (gbm_slot) gbm_slot[br] = -1;
+        }
+        return;
+      }
       int* keys = reinterpret_cast<int*>(bm);
       for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
       __syncthreads();
@@ -700,6 +710,16 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   if (T > a.hwords) {
     __syncthreads();
     return false;
+  }
+  if ((c_dbg & 256) && total <= SPARSE_NNZ_MAX) {
+    __syncthreads();
+    if (tid <= r1 - r0) {
+      const int64_t br = (int64_t)b * a.R + r0 + tid;
+      a.nslab[br] = 0;
+      a.cnt_br[br] = 0;
+      if (a.gbm_slot) a.gbm_slot[br] = -1;
+    }
+    return true;
   }
   int* keys = reinterpret_cast<int*>(L.bm);
   for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
@@ -1534,12 +1554,12 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       while ((1LL << sl) < (int64_t)(rec.hi - rec.lo)) ++sl;
     const int bshift = sl > LOGNB ? sl - LOGNB : 0;
     // in-bucket offsets fit u16 for panel-group slabs (span <= 2^(plog+4) rows,
-    // bshift <= 15); whole-column bins (CMLEN) use them while bshift <= 16
+    // bshift <= 15, 17 for groups of 64 panels); every slab uses them while bshift <= 16
     constexpr bool MOFF = L::MOFF_FITS && CBG_EMIT_MOFF;
-    if (MOFF && CBG_EMIT_REG && (!CMLEN || bshift <= 16))
+    if (MOFF && CBG_EMIT_REG && bshift <= 16)
       hash_emit_reg<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp,
                                reinterpret_cast<unsigned short*>(bv), out_ir, out_val, rec.obase);
-    else if (MOFF && (!CMLEN || bshift <= 16))
+    else if (MOFF && bshift <= 16)
       hash_emit_sorted<T, BS, NB, MOFF>(keys, vals, rec.lo, bshift, boff, cur, members, tmp, out_ir, out_val,
                                         rec.obase, reinterpret_cast<unsigned short*>(bv));
     else
@@ -2087,9 +2107,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const int64_t gp = ep ? atoll(ep) : GROUP_PRODUCTS;
     int64_t thr[NSMALL + NGCLS - 1];
     for (int i = 0; i < NSMALL; ++i) thr[i] = std::min(kSymThr[i], big);
+    static const char* el = getenv("CBG_GROUP_LOG_MAX");
+    const int glmax = el ? std::max(0, std::min(GROUP_LOG_MAX, atoi(el))) : GROUP_LOG_MAX;
     for (int c = 0; c + 1 < NGCLS; ++c) {
       const int64_t g = 1LL << (GROUP_LOG_MAX - c);
-      thr[NSMALL + c] = (groups && g <= bp.R) ? gp * bp.R / g : -1;
+      thr[NSMALL + c] = (groups && g <= bp.R && g <= (1LL << glmax)) ? gp * bp.R / g : -1;
     }
     BinPending sp;
     bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sp, s);

@@ -19,7 +19,15 @@ static size_t round_bytes(size_t b) {
     while (r < b) r <<= 1;
     return r;
   }
-  const size_t g = 2u << 20;
+  // 2 MiB granules up to 1 GiB; above, 1/16 of the size's power of two (<= 6.25 %
+  // rounding), so that the C arrays of consecutive MemEfficientSpGEMM phases --
+  // tens of GB whose sizes differ by a few percent -- reuse one cached block
+  // instead of each allocating another next to the cached one
+  size_t g = 2u << 20;
+  if (b >= ((size_t)1 << 30)) {
+    int l = 63 - __builtin_clzll(b);
+    g = (size_t)1 << (l - 4);
+  }
   return (b + g - 1) / g * g;
 }
 
@@ -41,9 +49,15 @@ void* DevicePool::alloc(size_t bytes) {
   }
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, rb);
+  // out of memory: release cached blocks largest first until the request fits
+  // (dropping the whole cache would make every later request allocate again)
+  while (e != hipSuccess && release_largest_cached()) {
+    (void)hipGetLastError();
+    e = hipMalloc(&p, rb);
+  }
   if (e != hipSuccess) {
     (void)hipGetLastError();
-    trim();  // drop the cache and retry once
+    trim();  // drop the cache (growable blocks included) and retry once
     e = hipMalloc(&p, rb);
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -55,6 +69,16 @@ void* DevicePool::alloc(size_t bytes) {
   live_[p] = rb;
   in_use_ += rb;
   return p;
+}
+
+bool DevicePool::release_largest_cached() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (free_.empty()) return false;
+  auto it = std::prev(free_.end());
+  (void)hipFree(it->second);
+  cached_ -= it->first;
+  free_.erase(it);
+  return true;
 }
 
 void DevicePool::free(void* p) {

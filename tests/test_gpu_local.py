@@ -139,14 +139,13 @@ def test_slab_value_narrowing(cbg, kind):
             assert_tiles_equal(C.to_host(), ref)
 
 
-def _panel_group_operands():
+def _panel_group_operands(m=(1 << 20) + 77):
     """Tall A (m = 2^20 + 77: 5 row panels of 2^18, the last one partial) and a B whose
     columns land in every big-column class: panel groups of 4 and 2 (expected products
     per group <= 4096), single-panel hash pairs, bitmap pairs, a group with > 512 B
     entries, and groups whose products crowd into one panel (nnz > one hash slab), which
     must fall back to per-panel slabs."""
     rng = np.random.default_rng(11)
-    m = (1 << 20) + 77
     heavy, light, local = 3000, 1000, 200  # A columns: 100 rows anywhere / 8 rows / 100 rows in panel 0
 
     def col(nr, hi):
@@ -188,6 +187,18 @@ def test_panel_groups_tall_matrix(cbg, sr):
     C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr)
     assert cbg.last_stats()["n_big"] > 300
     assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh, sr))
+
+
+def test_panel_groups_65_panels(cbg):
+    """m = 2^24 + 77 (65 row panels, the scale-24 case): columns of 4400-4800 products
+    fall in the 32-panel group class (groups of up to 64 panels, GROUP_LOG_MAX = 6),
+    one hash slab spanning 2^23 rows whose emit buckets need 17-bit row offsets;
+    bit-exact against the oracle, plus-times and min-plus."""
+    Ah, Bh = _panel_group_operands((1 << 24) + 77)
+    for sr in ("plus", "minplus"):
+        C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr)
+        assert cbg.last_stats()["n_big"] > 300
+        assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh, sr))
 
 
 def test_panel_groups_rmat20():
