@@ -365,7 +365,7 @@ def main():
                                 "plan_ms_per_step": [round(p_["plan_ms"], 2) for p_ in plans[-a.steps:]],
                                 "rule": "MemEfficientSpGEMM(phases=0): flops of the rank's product from tile count "
                                         "vectors (x the compression of an exact symbolic of a sample when the flops "
-                                        "bound asks for > 1 phase), 12 B per entry against half of the free HBM, "
+                                        "bound asks for > 1 phase), 12 B per entry against 60 % of the free HBM, "
                                         "inside each timed step"}
                                if plans else None),
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],

@@ -134,14 +134,17 @@ struct BinThr {
 
 // mode 0: key = flops; mode 1: key = (flops > big) ? +inf : cnt
 __global__ void k_classify(int64_t n, const int64_t* __restrict__ flops, const int32_t* __restrict__ cnt, int mode,
-                           int64_t big, BinThr thr, uint8_t* __restrict__ bin, int* __restrict__ hist) {
+                           int64_t big, BinThr thr, uint8_t* __restrict__ bin, int* __restrict__ hist,
+                           int64_t fused_max = 0) {
   __shared__ int lh[MAXBINS];
   if (threadIdx.x < MAXBINS) lh[threadIdx.x] = 0;
   __syncthreads();
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) {
     int64_t key = flops[i];
-    if (mode == 1) key = (key > big) ? INT64_MAX : (int64_t)cnt[i];
+    // numeric bins: big columns last; columns computed by the fused small-column
+    // pass (0 < flops <= fused_max) in bin 0, which the numeric skips
+    if (mode == 1) key = (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
     int b = thr.nb - 1;
     for (int j = 0; j < thr.nb - 1; ++j)
       if (key <= thr.t[j]) { b = j; break; }
@@ -1050,6 +1053,101 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
   }
 }
 
+// Small columns in ONE pass (flops <= 32 or <= 128: the first two symbolic
+// bins): a column with F products has at most F nonzeros, so its whole product
+// -- hash accumulate, sort -- runs in the symbolic phase into a temporary slot
+// of FMAX = the bin's flops bound entries (idx * FMAX: no scan needed), and the
+// count goes to cnt[col].  After the column pointers are known, k_copy_fused
+// moves each slot's entries to C.  The symbolic hash pass of these columns
+// (estimateNNZ_Hash for them) disappears; the temporary costs 24 B per entry.
+// GalerkinNew's products (mostly columns of <= 32 products) are dominated by it.
+template <int LOGT, int SR, int FMAX>
+__global__ __launch_bounds__(256) void k_fused_wave(const int32_t* __restrict__ perm, int n,
+                                                    const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                    const double* __restrict__ valB, const int2* __restrict__ cmap,
+                                                    const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ tir,
+                                                    double* __restrict__ tval) {
+  constexpr int T = 1 << LOGT;
+  static_assert(T >= 2 * FMAX || T == WAVE, "table sizes of the symbolic bins");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = threadIdx.x / WAVE, lane = lane_id();
+  char* base = smem + w * NumWaveLds<LOGT>::BYTES;
+  double* vals = reinterpret_cast<double*>(base);
+  double* bv = vals + T;
+  int* keys = reinterpret_cast<int*>(bv + WAVE);
+  int* pref = keys + T;
+  int* st = pref + WAVE + 4;
+  const int idx = blockIdx.x * (blockDim.x / WAVE) + w;
+  if (idx >= n) return;
+  const int col = perm[idx];
+  for (int j = lane; j < T; j += WAVE) {
+    keys[j] = EMPTY_KEY;
+    vals[j] = Sem<SR>::identity();
+  }
+  const int64_t p1 = cpB[col + 1];
+  for (int64_t c0 = cpB[col]; c0 < p1; c0 += WAVE) {
+    const int64_t p = c0 + lane;
+    int s = 0, len = 0;
+    double bval = 0.0;
+    if (p < p1) {
+      int2 e = cmap[irB[p]];
+      s = e.x;
+      len = e.y;
+      bval = valB[p];
+    }
+    const int incl = wave_incl_scan(len);
+    const int total = wave_last(incl);
+    pref[lane + 1] = incl;
+    if (lane == 0) pref[0] = 0;
+    st[lane] = seg_stage(s, incl - len);
+    bv[lane] = bval;
+    wave_sync();
+    wave_products(
+        pref, WAVE, 0, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
+        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
+        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
+    wave_sync();
+  }
+  const int64_t o = (int64_t)idx * FMAX;
+  if constexpr (T == WAVE) {  // one slot per lane: sort in registers
+    int key = keys[lane];
+    double val = vals[lane];
+    const int nout = __popcll(__ballot(key != EMPTY_KEY));
+    wave_bitonic_sort_kv(key, val, lane);
+    if (lane < nout) {
+      tir[o + lane] = key;
+      tval[o + lane] = val;
+    }
+    if (lane == 0) cnt[col] = nout;
+    return;
+  }
+  int nout = 0;
+  for (int j = lane; j < T; j += WAVE) nout += __popcll(__ballot(keys[j] != EMPTY_KEY));
+  bitonic_sort_kv<T, WAVE>(keys, vals, lane, WaveSync());
+  for (int e = lane; e < nout; e += WAVE) {
+    tir[o + e] = keys[e];
+    tval[o + e] = vals[e];
+  }
+  if (lane == 0) cnt[col] = nout;
+}
+// slot idx of a fused bin -> C at colptr[col] (FMAX threads per column)
+template <int FMAX>
+__global__ void k_copy_fused(const int32_t* __restrict__ perm, int n, const int32_t* __restrict__ cnt,
+                             const int64_t* __restrict__ colptr, const int32_t* __restrict__ tir,
+                             const double* __restrict__ tval, int32_t* __restrict__ out_ir,
+                             double* __restrict__ out_val) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t idx = t / FMAX;
+  const int e = (int)(t % FMAX);
+  if (idx >= n) return;
+  const int col = perm[idx];
+  if (e < cnt[col]) {
+    st_stream(&out_ir[colptr[col] + e], tir[idx * FMAX + e]);
+    st_stream(&out_val[colptr[col] + e], tval[idx * FMAX + e]);
+  }
+}
+
 // numeric: block per column
 template <int LOGT, int BS>
 struct NumBlockLds {
@@ -1653,6 +1751,15 @@ static void launch_sym_wave(const int32_t* perm, int n, const cbg_tile& B, const
   set_lds(k_sym_wave<LOGT>, lds);
   hipLaunchKernelGGL(k_sym_wave<LOGT>, dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, cmap, A.ir, cnt);
 }
+template <int LOGT, int SR, int FMAX>
+static void launch_fused(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
+                         int32_t* cnt, int32_t* tir, double* tval, hipStream_t s) {
+  if (n <= 0) return;
+  const size_t lds = 4 * NumWaveLds<LOGT>::BYTES;
+  set_lds(k_fused_wave<LOGT, SR, FMAX>, lds);
+  hipLaunchKernelGGL((k_fused_wave<LOGT, SR, FMAX>), dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, B.val,
+                     cmap, A.ir, A.val, cnt, tir, tval);
+}
 template <int LOGT, int BS>
 static void launch_sym_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
                              int32_t* cnt, hipStream_t s) {
@@ -1866,14 +1973,14 @@ struct BinPending {
   std::vector<int> h;
 };
 static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
-                         int nthr, int64_t big, BinPending& bp, hipStream_t s) {
+                         int nthr, int64_t big, BinPending& bp, hipStream_t s, int64_t fused_max = 0) {
   bp.bt.nb = nthr + 1;
   for (int i = 0; i < nthr; ++i) bp.bt.t[i] = thr[i];
   bp.bin.reset(n);
   bp.hist.reset(2 * MAXBINS);
   CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
   hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt, bp.bin.p,
-                     bp.hist.p);
+                     bp.hist.p, fused_max);
   bp.h.assign(MAXBINS, 0);
   CBG_HIP(hipMemcpyAsync(bp.h.data(), bp.hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
 }
@@ -2119,12 +2226,32 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     bin_scatter(nz, sp, sb, s, df);
   }
   // small-column symbolic bins on the side stream, big columns on the main one
+  // (bins 1-2 fused with their numeric unless CBG_FUSE_SMALL=0)
+  static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
+  const bool fused = fuse_small;
+  DBuf<int32_t> fused_ir;
+  DBuf<double> fused_val;
   fork(s);
   {
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
-    launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, ssym);
-    launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, ssym);
+    if (fused) {
+      // bins 1-2 (flops <= 32, <= 128): symbolic and numeric in one pass into fused_ir/val
+      fused_ir.reset((size_t)sb.count[1] * 32 + (size_t)sb.count[2] * 128 + 1);
+      fused_val.reset((size_t)sb.count[1] * 32 + (size_t)sb.count[2] * 128 + 1);
+      if (semiring == CBG_MIN_PLUS) {
+        launch_fused<6, 1, 32>(at(1), sb.count[1], B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p, ssym);
+        launch_fused<8, 1, 128>(at(2), sb.count[2], B, cmap.p, A, cnt.p, fused_ir.p + (size_t)sb.count[1] * 32,
+                                fused_val.p + (size_t)sb.count[1] * 32, ssym);
+      } else {
+        launch_fused<6, 0, 32>(at(1), sb.count[1], B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p, ssym);
+        launch_fused<8, 0, 128>(at(2), sb.count[2], B, cmap.p, A, cnt.p, fused_ir.p + (size_t)sb.count[1] * 32,
+                                fused_val.p + (size_t)sb.count[1] * 32, ssym);
+      }
+    } else {
+      launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, ssym);
+      launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, ssym);
+    }
     launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, ssym);
     launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, ssym);
     launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, ssym);
@@ -2226,7 +2353,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   BinPending npend;
-  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s);
+  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[2] : 0);
   // compaction of C's columns (SpDCCols(SpTuples): nonempty columns only)
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
@@ -2313,6 +2440,16 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   fork(s);
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
   else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
+  if (fused) {
+    const int32_t* P = sb.perm.p;
+    if (sb.count[1] > 0)
+      hipLaunchKernelGGL(k_copy_fused<32>, dim3(nblk((int64_t)sb.count[1] * 32, 256)), dim3(256), 0, snum,
+                         P + sb.offset[1], sb.count[1], cnt.p, colptr.p, fused_ir.p, fused_val.p, C.ir, C.val);
+    if (sb.count[2] > 0)
+      hipLaunchKernelGGL(k_copy_fused<128>, dim3(nblk((int64_t)sb.count[2] * 128, 256)), dim3(256), 0, snum,
+                         P + sb.offset[2], sb.count[2], cnt.p, colptr.p, fused_ir.p + (size_t)sb.count[1] * 32,
+                         fused_val.p + (size_t)sb.count[1] * 32, C.ir, C.val);
+  }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);

@@ -943,12 +943,12 @@ int summa_spgemm(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gn
 //    column counts of A's tiles (allgathered along the grid row) and the row
 //    counts of B's tiles (along the grid column): count vectors, not tiles;
 //  * nnz(C) <= flops; the compression nnz/flops is measured by an exact
-//    symbolic of a sample of the product (one rank: every 128th column of B, ~1/128
+//    symbolic of a sample of the product (one rank: every 256th column of B, ~1/256
 //    of a symbolic pass; a grid: every 8th row of the A block row times every
 //    16th column of the B block column, gathered like the SUMMA's tiles) and the
 //    estimate is flops x ratio x 1.1 -- only where the flops bound alone asks for
 //    more than one phase on some rank;
-//  * the C bytes a phase may take: CBG_PHASE_MEM_FRAC (0.5) of the memory left
+//  * the C bytes a phase may take: CBG_PHASE_MEM_FRAC (0.6) of the memory left
 //    after the tiles the SUMMA gathers -- perProcessMemory (GB, like the
 //    reference) when given, else the device's free memory plus libcbg's pool
 //    cache -- which leaves room for the symbolic bitmaps (<= 1/4 of the free
@@ -964,8 +964,8 @@ PhasePlan& phase_plan() {
 
 static double phase_mem_frac() {
   static const char* e = getenv("CBG_PHASE_MEM_FRAC");
-  const double f = e ? atof(e) : 0.5;
-  return f > 0 && f <= 1 ? f : 0.5;
+  const double f = e ? atof(e) : 0.6;
+  return f > 0 && f <= 1 ? f : 0.6;
 }
 
 static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t K, int64_t mem_gb, int64_t n_min,
@@ -1038,7 +1038,7 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   double ratio = 1.0;
   if (need_sample) {
     static const char* es = getenv("CBG_PHASE_SAMPLE");
-    const int cstride = es ? std::max(1, atoi(es)) : (g->nranks == 1 ? 128 : 16);
+    const int cstride = es ? std::max(1, atoi(es)) : (g->nranks == 1 ? 256 : 16);
     const int rstride = g->nranks == 1 ? 1 : 8;
     TileGuard As, Bs;
     rc = agree(g, step([&] {

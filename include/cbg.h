@@ -233,9 +233,9 @@ int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile
  * when per_process_memory_gb > 0 (or phases <= 0) the phase count comes from
  * memory: the flops of this rank's product (from the column counts of A's tiles
  * and the row counts of B's tiles, allgathered along the grid row / column), an
- * nnz(C) estimate (flops, times the compression of an exact symbolic of every
- * 64th column of B on one rank), and half of the memory left after the tiles the
- * SUMMA gathers -- perProcessMemory, or the device's free memory when it is 0;
+ * nnz(C) estimate (flops, times the compression of an exact symbolic of a sample
+ * of the product when the flops bound asks for more than one phase), and 60 % of
+ * the memory left after the tiles the SUMMA gathers -- perProcessMemory, or the device's free memory when it is 0;
  * the maximum over the grid.  If that memory is already taken by the inputs the
  * given phases are kept, like the reference. */
 int cbg_summa_spgemm_memeff(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,

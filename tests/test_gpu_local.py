@@ -445,12 +445,15 @@ def test_auto_phases_plan(cbg):
         d = _add(parts)
         assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (gd["nnz"], gd["hs"], gd["hv"], 0), kw
         assert plan["automatic"] and plan["flops"] == st["flops"] == G["rmat"]["s18_ef16"]["symbolic"]["flops"]
-        assert 0.8 * gd["nnz"] <= plan["nnz_est"] <= 1.3 * gd["nnz"], plan
         if kw:
-            # 2 GB minus the inputs, half of it for C: 12 B x 4.3e8 entries needs several phases
-            assert plan["phases"] >= 4 and plan["c_budget_bytes"] < 1e9, plan
+            # 2 GB minus the inputs, 60 % of it for C: 12 B x 4.3e8 entries needs several
+            # phases; the flops bound alone asks for more than one, so the compression was
+            # sampled and the estimate is close to the true nnz(C)
+            assert plan["phases"] >= 4 and plan["c_budget_bytes"] < 1.2e9, plan
+            assert 0.8 * gd["nnz"] <= plan["nnz_est"] <= 1.3 * gd["nnz"], plan
         else:
-            assert plan["phases"] == 1, plan
+            # the flops bound (12 B x 1.1e9) fits the device: one phase, no sample taken
+            assert plan["phases"] == 1 and plan["nnz_est"] == plan["flops"], plan
     A.tile.free()
     B.tile.free()
     grid.destroy()
