@@ -182,12 +182,31 @@ def main():
         for M in (X, Y, W):
             M.tile.free()
 
+    # algorithmic bytes of the full restriction (per local multiply:
+    # 16 F + 12 nnz(C) + 32 nnz(B) + 8 ncol(B)), from the two products' statistics
+    def alg_bytes():
+        X = cbg.PSpGEMM(A, T)
+        s1 = cbg.last_stats()
+        Y = cbg.PSpGEMM(S, X)
+        s2 = cbg.last_stats()
+        b = (16 * s1["flops"] + 12 * s1["nnz"] + 32 * T.tile.nnz + 8 * T.tile.n +
+             16 * s2["flops"] + 12 * s2["nnz"] + 32 * X.tile.nnz + 8 * X.tile.n)
+        X.tile.free()
+        Y.tile.free()
+        return b, s1["flops"] + s2["flops"]
+
+    bytes_alg, flops_full = alg_bytes()
     t_full = timed(full)
     t_split = timed(split)
     out = {"workload": "GalerkinNew R*A*R^T (R-MAT scale %d, restriction order %d)" % (a.scale, a.order),
            "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols), "n_gpus": world, "nnz_A": A.getnnz(),
            "nnz_T": T.getnnz(), "nnz_SAT": nnz_sat, "splitting_correct": bool(split_ok),
-           "full_restriction_s": t_full, "split_restriction_s": t_split}
+           "full_restriction_s": t_full, "split_restriction_s": t_split,
+           "roofline_full": {"bytes_alg_rank0": bytes_alg, "flops_rank0": flops_full,
+                             "achieved_GBps": bytes_alg / t_full / 1e9, "peak_GBps": 8000.0,
+                             "frac": bytes_alg / t_full / 8e12,
+                             "note": "both products' algorithmic bytes over the full restriction's wall time "
+                                     "(host-timed, max over ranks)"}}
     if a.minplus:
         out["full_restriction_minplus_s"] = timed(lambda: full(cbg.MinPlusSRing))
     if a.rank_tiles and world == 1:
