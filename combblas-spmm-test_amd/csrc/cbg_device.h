@@ -37,6 +37,24 @@ __device__ __forceinline__ T ld_stream(const T* p) {
   return *p;
 #endif
 }
+// 16-byte nontemporal store / load of 4 words (p 16-byte aligned)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_stream4(unsigned* p, uint4 v) {
+  u32x4 x = {v.x, v.y, v.z, v.w};
+#if CBG_NT_OUT
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+#else
+  *reinterpret_cast<u32x4*>(p) = x;
+#endif
+}
+__device__ __forceinline__ uint4 ld_stream4(const unsigned* p) {
+#if CBG_NT_OUT
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+  const u32x4 x = *reinterpret_cast<const u32x4*>(p);
+#endif
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
 template <class T>
 __device__ __forceinline__ void st_emit(T* p, T v) {
 #if CBG_NT_EMIT

@@ -531,7 +531,8 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
         return;
       }
       int* keys = reinterpret_cast<int*>(bm);
-      for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
+      for (int j = tid; j < T / 4; j += BS)
+        reinterpret_cast<int4*>(keys)[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
       __syncthreads();
       int count = 0;
       if (!(c_dbg & 64))
@@ -558,7 +559,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       phase_mark(tmark, 9);
       return;
     }
-    for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
+    for (int j = tid; j < pwords / 4; j += BS) reinterpret_cast<uint4*>(bm)[j] = make_uint4(0u, 0u, 0u, 0u);
     if (tid < NFINE_MAX) fine[tid] = 0;
     __syncthreads();
     if (!(c_dbg & 1))
@@ -568,7 +569,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
           [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
     __syncthreads();
   } else {
-  for (int j = tid; j < pwords; j += BS) bm[j] = 0u;
+  for (int j = tid; j < pwords / 4; j += BS) reinterpret_cast<uint4*>(bm)[j] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < NFINE_MAX) fine[tid] = 0;
   __syncthreads();
   for (int64_t c0 = p0; c0 < p1; c0 += BS) {    const int64_t p = c0 + tid;
@@ -616,17 +617,20 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   {
     // wave w owns the fine ranges w, w + 8, ...: its lanes read (and store)
     // 64 consecutive words per step, and one wave reduction per fine range
+    // (16-byte vectors: a lane takes 4 consecutive words; words past the
+    // panel's end are the zeroed tail of the bitmap)
     constexpr int FW = 1 << (FINE_LOG - 5);  // words per fine range
+    static_assert(FW % (4 * WAVE) == 0, "fine range of whole 16-byte lane vectors");
     const int w = tid / WAVE, lane = lane_id();
     for (int f = w; f * FW < words; f += BS / WAVE) {
       int c = 0;
 #pragma unroll
-      for (int q = 0; q < FW; q += WAVE) {
-        const int j = f * FW + q + lane;
+      for (int q = 0; q < FW; q += 4 * WAVE) {
+        const int j = f * FW + q + 4 * lane;
         if (j < words) {
-          const unsigned x = bm[j];
-          if (gdst && !(c_dbg & 128)) st_stream(&gdst[j], x);
-          c += __popc(x);
+          const uint4 x = *reinterpret_cast<const uint4*>(bm + j);
+          if (gdst && !(c_dbg & 128)) st_stream4(&gdst[j], x);
+          c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
         }
       }
       c = wave_sum(c);
@@ -725,7 +729,8 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
     return true;
   }
   int* keys = reinterpret_cast<int*>(L.bm);
-  for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
+  for (int j = tid; j < T / 4; j += BS)
+    reinterpret_cast<int4*>(keys)[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
   if (tid == 0) L.fine[0] = 0;
   __syncthreads();
   int count = 0;
@@ -854,8 +859,8 @@ struct __attribute__((aligned(16))) SlabRec {
   int lo, hi;     // row range
   int nout;       // nnz of the slab
   int slot;       // kept symbolic bitmap (-1: none)
-  int full;       // the slab is its whole panel
-  int pad;
+  int full;       // A's whole panel runs are the slab's products (the slab is its panel, or its pair's only slab)
+  int ends;       // bit 0: first slab of its (column, panel) pair, bit 1: last
 };
 
 #ifndef CBG_HASH_LOAD_NUM  // numeric hash slab tables: T >= (NUM/DEN) * nnz
@@ -970,8 +975,10 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
       rec.hi = d.y;
       rec.nout = d.w & (SLAB_SPARSE - 1);
       rec.slot = gbm_slot ? gbm_slot[br] : -1;
-      rec.full = (d.x == R0 && d.y == R1);
-      rec.pad = 0;
+      // a pair's only slab holds every row its products reach (the plan trims
+      // empty fine ranges only), so A's whole panel runs are its products
+      rec.full = (d.x == R0 && d.y == R1) || nslab[br] == 1;
+      rec.ends = (s == 0 ? 1 : 0) | (s == nslab[br] - 1 ? 2 : 0);
       list[lb[key] + atomicAdd(&lc[key], 1)] = rec;
     }
   }
@@ -1298,8 +1305,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   const int wslot = 1 << (plog - 5);
   int i = blockIdx.x;
   if (i >= n) return;
-  // prefetch registers (bitmap words are coalesced: word k*BS + tid)
-  unsigned pw[WPT];
+  // prefetch registers (bitmap words in 16-byte lane vectors: words 4 (k*BS + tid) .. +3)
+  constexpr int WV = WPT / 4;
+  uint4 pw[WV];
   int p_ir = 0;
   double p_bv = 0.0;
   int2 p_ce = make_int2(0, 0);
@@ -1310,9 +1318,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const unsigned* src = gbm + (int64_t)r.slot * wslot + ((r.lo - (r.r << plog)) >> 5);
     const int words = rec_words(r);
 #pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-      const int j = k * BS + tid;
-      pw[k] = j < words ? ld_stream(&src[j]) : 0u;
+    for (int k = 0; k < WV; ++k) {
+      const int j = 4 * (k * BS + tid);
+      if (j + 3 < words) {
+        pw[k] = ld_stream4(src + j);
+      } else {  // the slab's last partial vector (never past the slab's words)
+        pw[k] = make_uint4(j < words ? ld_stream(&src[j]) : 0u, j + 1 < words ? ld_stream(&src[j + 1]) : 0u,
+                           j + 2 < words ? ld_stream(&src[j + 2]) : 0u, 0u);
+      }
     }
   };
   auto fetch_stage1 = [&](const SlabRec& r) {
@@ -1348,9 +1361,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
     unsigned long long tmark = wall_clock64();
 #pragma unroll
-    for (int k = 0; k < WPT; ++k) {
-      const int j = k * BS + tid;
-      if (j < words) bm[j] = have_bm ? pw[k] : 0u;
+    for (int k = 0; k < WV; ++k) {
+      const int j = 4 * (k * BS + tid);
+      if (j < words) *reinterpret_cast<uint4*>(bm + j) = have_bm ? pw[k] : make_uint4(0u, 0u, 0u, 0u);
     }
     if (CBG_VEC_INIT) {  // 16-byte LDS stores (CAP is even, vals is 16-byte aligned)
       const double id = Sem<SR>::identity();
@@ -1430,8 +1443,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
               s = ce.x;
               len = ce.y - ce.x;
             } else if (ce.y > ce.x) {
-              const int a = lower_bound_g(irA, ce.x, ce.y, lo);
-              const int z = lower_bound_g(irA, a, ce.y, hi);
+              // the pair's first slab starts at its run's start, the last ends at its end
+              const int a = (rec.ends & 1) ? ce.x : lower_bound_g(irA, ce.x, ce.y, lo);
+              const int z = (rec.ends & 2) ? ce.y : lower_bound_g(irA, a, ce.y, hi);
               s = a;
               len = z - a;
             }
@@ -1806,7 +1820,7 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
   r.nout = (int)(colptr[col + 1] - r.obase);
   r.slot = -1;
   r.full = 1;
-  r.pad = 0;
+  r.ends = 3;
   rec[i] = r;
 }
 

@@ -10,7 +10,7 @@ name=$1; shift
 out=../build/variants/$name
 mkdir -p $out
 FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../include -Wall -Wno-unused-function -Wno-unused-variable"
-/opt/rocm/bin/hipcc $FLAGS $* -c csrc/cbg_local.hip -o $out/cbg_local.o
+/opt/rocm/bin/hipcc $FLAGS $* -c ${SRC:-csrc/cbg_local.hip} -o $out/cbg_local.o
 objs=$(ls build/*.o | grep -v cbg_local.o)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/libcbg.so $out/cbg_local.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo $out/libcbg.so
