@@ -39,7 +39,8 @@ __device__ unsigned long long g_phase[16];
 //   64: k_sym_panel skips the hash-count products of sparse pairs and panel groups
 //  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
 //  256: k_sym_panel leaves a hash-mode pair or panel group right after its staging
-__device__ unsigned long long g_stat[8];
+//  512: k_num_slab_hash skips its products       1024: k_num_slab_hash skips its emit
+__device__ unsigned long long g_stat[12];  // [4] bitmap slab products, [7] panel hash, [8] column hash products, [9] hash nnz
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
   if ((c_dbg & 16) && threadIdx.x == 0) {
     const unsigned long long n = wall_clock64();
@@ -361,7 +362,10 @@ constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= ma
 #define CBG_BIG_BS 512
 #endif
 constexpr int BIG_BS = CBG_BIG_BS;
-constexpr int SPARSE_SLAB_MAX = 4096;   // products of a (column, panel) pair counted by hash -> hash slab
+#ifndef CBG_SPARSE_SLAB_MAX
+#define CBG_SPARSE_SLAB_MAX 4096
+#endif
+constexpr int SPARSE_SLAB_MAX = CBG_SPARSE_SLAB_MAX;  // products of a (column, panel) pair counted by hash -> hash slab
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 
 // Panel column maps of A: cmapP[r * (n+1) + k] = (first, end) of column k's
@@ -1461,6 +1465,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
         } else {
           total = pref[BS];
         }
+        if ((c_dbg & 32) && pass == 1 && tid == 0) atomicAdd(&g_stat[4], (unsigned long long)total);
         if (!(c_dbg & (2 << pass))) slab_products<SR, BS, VA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
@@ -1653,6 +1658,8 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       __syncthreads();
       phase_mark(tmark, 13);
       if (c == nch - 1 && has_next) fetch1(nrec);
+      if ((c_dbg & 32) && tid == 0) atomicAdd(&g_stat[CMLEN ? 8 : 7], (unsigned long long)total);
+      if (!(c_dbg & 512))
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
           [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
@@ -1661,6 +1668,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       phase_mark(tmark, 14);
     }
     if (has_next) fetch2(nrec);
+    if ((c_dbg & 32) && tid == 0) atomicAdd(&g_stat[9], (unsigned long long)rec.nout);
     int sl = plog;  // emit buckets span 2^sl rows from lo (a panel group spans several panels)
     if (!CMLEN)
       while ((1LL << sl) < (int64_t)(rec.hi - rec.lo)) ++sl;
@@ -1668,7 +1676,9 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
     // in-bucket offsets fit u16 for panel-group slabs (span <= 2^(plog+4) rows,
     // bshift <= 15, 17 for groups of 64 panels); every slab uses them while bshift <= 16
     constexpr bool MOFF = L::MOFF_FITS && CBG_EMIT_MOFF;
-    if (MOFF && CBG_EMIT_REG && bshift <= 16)
+    if (c_dbg & 1024)
+      ;
+    else if (MOFF && CBG_EMIT_REG && bshift <= 16)
       hash_emit_reg<T, BS, NB>(keys, vals, rec.lo, bshift, boff, cur, members, tmp,
                                reinterpret_cast<unsigned short*>(bv), out_ir, out_val, rec.obase);
     else if (MOFF && bshift <= 16)
@@ -1806,7 +1816,7 @@ static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, cons
 
 // records of the block hash bins: a column is a hash slab over all rows
 __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int64_t* __restrict__ cpB,
-                              const int64_t* __restrict__ colptr, SlabRec* __restrict__ rec) {
+                              const int64_t* __restrict__ colptr, int m, SlabRec* __restrict__ rec) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int col = perm[i];
@@ -1816,7 +1826,7 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
   r.nb = (int)(cpB[col + 1] - r.p0);
   r.r = 0;
   r.lo = 0;
-  r.hi = 0;
+  r.hi = m;  // the rows the slab spans
   r.nout = (int)(colptr[col + 1] - r.obase);
   r.slot = -1;
   r.full = 1;
@@ -1826,26 +1836,30 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
 
 template <int LOGT, int BS, int SR>
 static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
-                                  const cbg_tile& A, const int64_t* colptr, cbg_tile& C, hipStream_t s,
-                                  DeferredFree& df) {
+                                  const cbg_tile& A, const float* valAf, const int64_t* colptr, cbg_tile& C,
+                                  hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   DBuf<SlabRec> rec(n);
-  hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, rec.p);
+  hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, (int)A.m, rec.p);
   constexpr int L = SlabHashLds<1 << LOGT, BS>::BYTES;
-  auto k = k_num_slab_hash<SR, 1 << LOGT, BS, true>;
-  set_lds(k, L);
-  static int per_cu = 0;
-  if (!per_cu) {
-    CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-    if (per_cu < 1) per_cu = 1;
-  }
   int lm = 0;
   while ((1LL << lm) < A.m) ++lm;  // emit buckets span [0, 2^lm)
-  const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap, (int64_t)0,
-                     A.ir, A.val, C.ir, C.val);
+  auto go = [&](auto k, const auto* valA, int& per_cu) {
+    set_lds(k, L);
+    if (!per_cu) {
+      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
+      if (per_cu < 1) per_cu = 1;
+    }
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap,
+                       (int64_t)0, A.ir, valA, C.ir, C.val);
+  };
+  // A's f32 values (exact, see k_vals_f32) when the big-column path made them
+  static int per_cu_d = 0, per_cu_f = 0;
+  if (valAf) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, float>, valAf, per_cu_f);
+  else go(k_num_slab_hash<SR, 1 << LOGT, BS, true, double>, A.val, per_cu_d);
   df.take(rec);
   df.take(queue);
 }
@@ -2028,8 +2042,8 @@ static bool block_bins_persistent() {
 }
 
 template <int SR>
-static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile& B, const int2* cmap,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
+static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* valAf, const cbg_tile& B,
+                             const int2* cmap, const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
   launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, s);
@@ -2037,10 +2051,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const cbg_tile
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
   if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s, df);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s, df);
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, s, df);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, s, df);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, s, df);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, s, df);
   } else {
     launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
     launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
@@ -2452,8 +2466,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bin_scatter(nz, npend, nbn, s, df);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
-  else numeric_dispatch<0>(nbn, A, B, cmap.p, colptr.p, C, snum, df);
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, snum, df);
+  else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, snum, df);
   if (fused) {
     const int32_t* P = sb.perm.p;
     if (sb.count[1] > 0)
@@ -2477,10 +2491,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16) {
       if (dbg & 32) {
-        unsigned long long gs[8];
+        unsigned long long gs[12];
         CBG_HIP(hipMemcpyFromSymbol(gs, HIP_SYMBOL(g_stat), sizeof(gs)));
-        std::fprintf(stderr, "[cbg k_num_slab] slabs %llu nonfull %llu nb %llu nb_nonfull %llu nout %llu multichunk %llu\n",
-                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6]);
+        std::fprintf(stderr, "[cbg k_num_slab] slabs %llu nonfull %llu nb %llu nb_nonfull %llu nout %llu multichunk %llu "
+                     "products %llu | hash products panel %llu column %llu nout %llu\n",
+                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6], gs[4], gs[7], gs[8], gs[9]);
         std::memset(gs, 0, sizeof(gs));
         CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stat), gs, sizeof(gs)));
       }
