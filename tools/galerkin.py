@@ -130,6 +130,8 @@ def main():
     p.add_argument("--order", type=int, default=2)
     p.add_argument("--iters", type=int, default=3)
     p.add_argument("--minplus", action="store_true")
+    p.add_argument("--only-full", action="store_true",
+                   help="time the full restriction only (kernel traces: its multiplies are the last dispatches)")
     p.add_argument("--rank-tiles", default=None,
                    help="RxC: time every rank's local products of a RxC grid on this one GPU (no communication)")
     a = p.parse_args()
@@ -197,7 +199,7 @@ def main():
 
     bytes_alg, flops_full = alg_bytes()
     t_full = timed(full)
-    t_split = timed(split)
+    t_split = None if a.only_full else timed(split)
     out = {"workload": "GalerkinNew R*A*R^T (R-MAT scale %d, restriction order %d)" % (a.scale, a.order),
            "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols), "n_gpus": world, "nnz_A": A.getnnz(),
            "nnz_T": T.getnnz(), "nnz_SAT": nnz_sat, "splitting_correct": bool(split_ok),
