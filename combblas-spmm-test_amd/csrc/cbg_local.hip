@@ -118,6 +118,115 @@ __global__ __launch_bounds__(256) void k_flops_tail(const int64_t* __restrict__ 
   }
 }
 
+// flops of every B column, load-balanced over B's ENTRIES (merge-path style):
+// block b takes entries [b*E, (b+1)*E), finds the column holding its first
+// entry with a wave-cooperative 64-ary search of cpB, marks where its other
+// columns start, and reduces each column's A lengths in LDS; a column cut by a
+// block boundary gets one global atomic per block.  Replaces a group of lanes
+// per column, whose serial walk over a column's entries (up to FLOP_HEAD, the
+// rest on a tail kernel) set the kernel's time on skewed B (GalerkinNew's A*T
+// columns: 0.69 ms; the hub tail of S*(AT): 0.39 ms).  Block sums go to
+// part[] and one block adds them up (a single-address atomic per block
+// serialized 60 K blocks).
+constexpr int FSEG_T = 256, FSEG_PER = 8, FSEG_E = FSEG_T * FSEG_PER;
+__global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB, const int64_t* __restrict__ cpB,
+                                                    const int32_t* __restrict__ irB, const int2* __restrict__ cmap,
+                                                    unsigned long long* __restrict__ flops,
+                                                    unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long lsum[FSEG_E];
+  __shared__ __attribute__((aligned(16))) int head[FSEG_E];  // columns starting at each entry (empty ones too)
+  __shared__ int tmp[FSEG_T / WAVE + 4];
+  __shared__ unsigned long long wsum[FSEG_T / WAVE];
+  __shared__ int64_t c_lo_s;
+  const int tid = threadIdx.x;
+  const int64_t e0 = blockIdx.x * (int64_t)FSEG_E;
+  const int64_t e1 = min(e0 + (int64_t)FSEG_E, nnzB);
+  if (tid < WAVE) {
+    // the largest c with cpB[c] <= e0 (cpB[0] = 0 <= e0 < cpB[nzcB] = nnzB)
+    int64_t lo = 0, hi = nzcB;
+    while (hi - lo > 1) {
+      const int64_t step = (hi - lo + WAVE - 1) / WAVE;
+      const int64_t idx = lo + (int64_t)tid * step;
+      const bool le = idx < hi && cpB[idx] <= e0;
+      const unsigned long long m = __ballot(le);  // lane 0 (idx = lo) is always set
+      const int64_t nlo = lo + (int64_t)(63 - __clzll((long long)m)) * step;
+      hi = min(nlo + step, hi);
+      lo = nlo;
+    }
+    if (tid == 0) c_lo_s = lo;
+  }
+  for (int i = tid; i < FSEG_E; i += FSEG_T) lsum[i] = 0ull;
+  for (int i = tid; i < FSEG_E / 4; i += FSEG_T) reinterpret_cast<int4*>(head)[i] = make_int4(0, 0, 0, 0);
+  __syncthreads();
+  const int64_t c_lo = c_lo_s;
+  // starts of the block's other columns (DCSC columns are nonempty: at most E
+  // of them; an empty column would count at its position like any other)
+  for (int64_t c = c_lo + 1 + tid; c < nzcB; c += FSEG_T) {
+    const int64_t p = cpB[c];
+    if (p >= e1) break;
+    atomicAdd(&head[p - e0], 1);
+  }
+  __syncthreads();
+  const int i0 = tid * FSEG_PER;
+  int hd[FSEG_PER];
+  {
+    const int4 a = *reinterpret_cast<const int4*>(head + i0), b = *reinterpret_cast<const int4*>(head + i0 + 4);
+    hd[0] = a.x, hd[1] = a.y, hd[2] = a.z, hd[3] = a.w, hd[4] = b.x, hd[5] = b.y, hd[6] = b.z, hd[7] = b.w;
+  }
+  static_assert(FSEG_PER == 8, "two int4 head reads per thread");
+  int hc = 0;
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) hc += hd[j];
+  int ncol;
+  int col = block_excl_scan<FSEG_T>(hc, tmp, &ncol);  // local column of entry i0, before its own head
+  int k[FSEG_PER];
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) k[j] = e0 + i0 + j < e1 ? irB[e0 + i0 + j] : -1;
+  int len[FSEG_PER];
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) len[j] = k[j] >= 0 ? cmap[k[j]].y : 0;
+  unsigned long long acc = 0, bsum = 0;
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) {
+    if (hd[j]) {
+      if (acc) atomicAdd(&lsum[col], acc);
+      acc = 0;
+      col += hd[j];
+    }
+    acc += (unsigned long long)len[j];
+    bsum += (unsigned long long)len[j];
+  }
+  if (acc) atomicAdd(&lsum[col], acc);
+  __syncthreads();
+  for (int t = tid; t <= ncol; t += FSEG_T) {
+    const unsigned long long v = lsum[t];
+    if (v) atomicAdd(&flops[c_lo + t], v);
+  }
+  bsum = (unsigned long long)wave_sum64((long long)bsum);
+  if (lane_id() == 0) wsum[tid / WAVE] = bsum;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < FSEG_T / WAVE; ++w) t += wsum[w];
+    part[blockIdx.x] = t;
+  }
+}
+// total of part[0, n) into *out (one block)
+__global__ __launch_bounds__(1024) void k_sum_parts(const unsigned long long* __restrict__ part, int64_t n,
+                                                    unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long ws[1024 / WAVE];
+  unsigned long long s = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) s += part[i];
+  s = (unsigned long long)wave_sum64((long long)s);
+  if (lane_id() == 0) ws[threadIdx.x / WAVE] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < 1024 / WAVE; ++w) t += ws[w];
+    *out = t;
+  }
+}
+
 // panel column map when A has a single row panel: {start, end} from cmap
 __global__ void k_colmap_panel1(int64_t nA1, const int2* __restrict__ cmap, int2* __restrict__ cmapP) {
   const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -127,50 +236,80 @@ __global__ void k_colmap_panel1(int64_t nA1, const int2* __restrict__ cmap, int2
   }
 }
 
-constexpr int MAXBINS = 16;
+constexpr int MAXBINS = 24;
 struct BinThr {
   int64_t t[MAXBINS];  // bin b <=> key <= t[b] (first match); last bin catches the rest
   int nb;
 };
 
-// mode 0: key = flops; mode 1: key = (flops > big) ? +inf : cnt
-__global__ void k_classify(int64_t n, const int64_t* __restrict__ flops, const int32_t* __restrict__ cnt, int mode,
-                           int64_t big, BinThr thr, uint8_t* __restrict__ bin, int* __restrict__ hist,
-                           int64_t fused_max = 0) {
+// mode 0: key = flops; mode 1: key = (flops > big) ? +inf : cnt.
+// A block takes BIN_ITEMS x 256 columns (strided, coalesced), so that the
+// per-block histogram atomics -- a few hundred blocks on 16 addresses -- do
+// not serialize (one block per 256 columns: 80 us for 2 M columns).
+constexpr int BIN_ITEMS = 16;
+// big_entries (mode 0, optional): B entries of the columns in bins >= big_bin
+__global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __restrict__ flops,
+                                                  const int32_t* __restrict__ cnt, int mode, int64_t big, BinThr thr,
+                                                  uint8_t* __restrict__ bin, int* __restrict__ hist,
+                                                  int64_t fused_max, const int64_t* __restrict__ cpB, int big_bin,
+                                                  unsigned long long* __restrict__ big_entries,
+                                                  unsigned long long* __restrict__ bin_flops) {
   __shared__ int lh[MAXBINS];
-  if (threadIdx.x < MAXBINS) lh[threadIdx.x] = 0;
-  __syncthreads();
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) {
-    int64_t key = flops[i];
-    // numeric bins: big columns last; columns computed by the fused small-column
-    // pass (0 < flops <= fused_max) in bin 0, which the numeric skips
-    if (mode == 1) key = (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
-    int b = thr.nb - 1;
-    for (int j = 0; j < thr.nb - 1; ++j)
-      if (key <= thr.t[j]) { b = j; break; }
-    bin[i] = (uint8_t)b;
-    atomicAdd(&lh[b], 1);
+  __shared__ unsigned long long lf[MAXBINS];
+  __shared__ unsigned long long lbe;
+  if (threadIdx.x < MAXBINS) {
+    lh[threadIdx.x] = 0;
+    lf[threadIdx.x] = 0;
   }
+  if (threadIdx.x == 0) lbe = 0;
+  __syncthreads();
+  unsigned long long be = 0;
+  const int64_t i0 = blockIdx.x * (int64_t)(256 * BIN_ITEMS) + threadIdx.x;
+#pragma unroll 4
+  for (int j = 0; j < BIN_ITEMS; ++j) {
+    const int64_t i = i0 + j * 256;
+    if (i < n) {
+      const int64_t f = flops[i];
+      int64_t key = f;
+      // numeric bins: big columns last; columns computed by the fused small-column
+      // pass (0 < flops <= fused_max) in bin 0, which the numeric skips
+      if (mode == 1) key = (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
+      int b = thr.nb - 1;
+      for (int q = 0; q < thr.nb - 1; ++q)
+        if (key <= thr.t[q]) { b = q; break; }
+      bin[i] = (uint8_t)b;
+      atomicAdd(&lh[b], 1);
+      if (f > 0) atomicAdd(&lf[b], (unsigned long long)f);
+      if (big_entries && b >= big_bin) be += (unsigned long long)(cpB[i + 1] - cpB[i]);
+    }
+  }
+  if (big_entries && be) atomicAdd(&lbe, be);
   __syncthreads();
   if (threadIdx.x < thr.nb && lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
+  if (threadIdx.x < thr.nb && lf[threadIdx.x]) atomicAdd(&bin_flops[threadIdx.x], lf[threadIdx.x]);
+  if (big_entries && threadIdx.x == 0 && lbe) atomicAdd(big_entries, lbe);
 }
 
-__global__ void k_bin_scatter(int64_t n, const uint8_t* __restrict__ bin, int nb, int* __restrict__ cursor,
-                              int32_t* __restrict__ perm) {
+__global__ __launch_bounds__(256) void k_bin_scatter(int64_t n, const uint8_t* __restrict__ bin, int nb,
+                                                     int* __restrict__ cursor, int32_t* __restrict__ perm) {
   __shared__ int lc[MAXBINS], lb[MAXBINS];
   if (threadIdx.x < MAXBINS) lc[threadIdx.x] = 0;
   __syncthreads();
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int b = -1, slot = 0;
-  if (i < n) {
-    b = bin[i];
-    slot = atomicAdd(&lc[b], 1);
+  const int64_t i0 = blockIdx.x * (int64_t)(256 * BIN_ITEMS) + threadIdx.x;
+  int b[BIN_ITEMS], slot[BIN_ITEMS];
+#pragma unroll
+  for (int j = 0; j < BIN_ITEMS; ++j) {
+    const int64_t i = i0 + j * 256;
+    b[j] = i < n ? bin[i] : -1;
   }
+#pragma unroll
+  for (int j = 0; j < BIN_ITEMS; ++j) slot[j] = b[j] >= 0 ? atomicAdd(&lc[b[j]], 1) : 0;
   __syncthreads();
   if (threadIdx.x < nb) lb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], lc[threadIdx.x]) : 0;
   __syncthreads();
-  if (i < n) perm[lb[b] + slot] = (int32_t)i;
+#pragma unroll
+  for (int j = 0; j < BIN_ITEMS; ++j)
+    if (b[j] >= 0) perm[lb[b[j]] + slot[j]] = (int32_t)(i0 + j * 256);
 }
 
 struct RowVal {
@@ -377,13 +516,9 @@ constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in
 // binary-searches each panel boundary (long ones) and writes its R entries,
 // so every store of a wave is one row of the map at consecutive columns
 // (coalesced; one thread per entry scattering over R rows was 3x slower).
-__global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
-                                    const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
-                                    int2* __restrict__ cmapP) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= nzcA) return;
-  const int64_t k = jcA[i];
-  const int a = (int)cpA[i], e = (int)cpA[i + 1];
+// A(:,k) = rows irA[a, e): its run inside every row panel, one thread
+__device__ __forceinline__ void panel_runs(const int32_t* __restrict__ irA, int a, int e, int plog, int R,
+                                           int64_t nA1, int64_t k, int2* __restrict__ cmapP) {
   int pos = a;
   for (int r = 0; r < R; ++r) {
     const int lo = pos;
@@ -398,6 +533,28 @@ __global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cp
       }
     }
     cmapP[r * nA1 + k] = make_int2(lo, pos);
+  }
+}
+__global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
+                                    const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
+                                    int2* __restrict__ cmapP) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nzcA) return;
+  panel_runs(irA, (int)cpA[i], (int)cpA[i + 1], plog, R, nA1, jcA[i], cmapP);
+}
+// the same for the A columns the big B columns reference only (a wave per big
+// column, a lane per entry; a column referenced twice is written twice alike)
+__global__ void k_colmap_panels_entries(const int32_t* __restrict__ perm_big, int nbig,
+                                        const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                        const int2* __restrict__ cmap, const int32_t* __restrict__ irA, int plog,
+                                        int R, int64_t nA1, int2* __restrict__ cmapP) {
+  const int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
+  if (w >= nbig) return;
+  const int col = perm_big[w];
+  for (int64_t p = cpB[col] + lane_id(); p < cpB[col + 1]; p += WAVE) {
+    const int k = irB[p];
+    const int2 e = cmap[k];
+    panel_runs(irA, e.x, e.x + e.y, plog, R, nA1, k, cmapP);
   }
 }
 
@@ -1142,20 +1299,216 @@ __global__ __launch_bounds__(256) void k_fused_wave(const int32_t* __restrict__ 
   }
   if (lane == 0) cnt[col] = nout;
 }
-// slot idx of a fused bin -> C at colptr[col] (FMAX threads per column)
-template <int FMAX>
-__global__ void k_copy_fused(const int32_t* __restrict__ perm, int n, const int32_t* __restrict__ cnt,
+// Small columns by expand-sort-compress in registers (flops <= fmax = 64 *
+// NPL / CPW per column): a wave takes CPW consecutive columns of its bin,
+// expands their <= 64 * NPL products (NPL per lane, product q in register q /
+// 64 of lane q % 64), sorts the (column, row) keys with their values across
+// the wave (bitonic), combines equal keys (segmented scan) and writes each
+// column's sorted entries to its temporary slot idx * fmax, and cnt[col] =
+// its nnz.  No LDS hash and no wave per column: GalerkinNew's columns carry 7
+// products on average, so a wave per column left 7/8 of its lanes idle through
+// every load of the column's chain.  key = c << SH | row needs A.m < 2^SH (the
+// host launches CPW = 1 when it is not).
+template <int NPL>
+__device__ __forceinline__ void wave_bitonic_sort_kvn(int (&key)[NPL], double (&val)[NPL], int lane) {
+  // element i = j * 64 + lane
+#pragma unroll
+  for (int k = 2; k <= WAVE * NPL; k <<= 1) {
+#pragma unroll
+    for (int d = k >> 1; d > 0; d >>= 1) {
+      if (d >= WAVE) {
+        const int dj = d / WAVE;
+#pragma unroll
+        for (int j = 0; j < NPL; ++j) {
+          if (j & dj) continue;
+          const int i = j * WAVE + lane;
+          const bool up = (i & k) == 0;
+          const int j2 = j | dj;
+          if (up ? key[j2] < key[j] : key[j2] > key[j]) {
+            const int tk = key[j];
+            key[j] = key[j2];
+            key[j2] = tk;
+            const double tv = val[j];
+            val[j] = val[j2];
+            val[j2] = tv;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NPL; ++j) {
+          const int i = j * WAVE + lane;
+          const int ok = __shfl_xor(key[j], d);
+          const double ov = __shfl_xor(val[j], d);
+          const bool up = (i & k) == 0;
+          const bool lower = (lane & d) == 0;
+          if (lower == up ? ok < key[j] : ok > key[j]) {
+            key[j] = ok;
+            val[j] = ov;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int CPW, int NPL, int SR>
+__global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ perm, int n, int fmax,
+                                                  const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
+                                                  const double* __restrict__ valB, const int2* __restrict__ cmap,
+                                                  const int32_t* __restrict__ irA, const double* __restrict__ valA,
+                                                  int32_t* __restrict__ cnt, int32_t* __restrict__ tir,
+                                                  double* __restrict__ tval, int64_t slot_base,
+                                                  int64_t* __restrict__ tslot) {
+  constexpr int LOGC = CPW <= 1 ? 0 : CPW <= 2 ? 1 : CPW <= 4 ? 2 : CPW <= 8 ? 3 : CPW <= 16 ? 4 : 5;
+  static_assert((1 << LOGC) == CPW && CPW <= 32, "columns per wave");
+  static_assert(NPL == 1 || NPL == 2 || NPL == 4, "products per lane");
+  constexpr int SH = 31 - LOGC;
+  const int lane = lane_id();
+  const int64_t idx0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE * CPW;
+  if (idx0 >= n) return;
+  int col = -1;
+  int64_t p0 = 0, p1 = 0;
+  if (lane < CPW && idx0 + lane < n) {
+    col = perm[idx0 + lane];
+    p0 = cpB[col];
+    p1 = cpB[col + 1];
+  }
+  const int nb = (int)(p1 - p0);
+  const int binc = wave_incl_scan(nb);  // B entries of columns 0..lane
+  const int bexc = binc - nb;
+  const int totalB = wave_last(binc);
+  int key[NPL];
+  double val[NPL];
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    key[j] = EMPTY_KEY;
+    val[j] = 0.0;
+  }
+  int pbase = 0;  // products placed so far (element index)
+  for (int e0 = 0; e0 < totalB; e0 += WAVE) {
+    const int e = e0 + lane;
+    int c = 0;  // column of B entry e
+#pragma unroll
+    for (int cc = 1; cc < CPW; ++cc) c += __builtin_amdgcn_readlane(bexc, cc) <= e ? 1 : 0;
+    const int ex_c = __shfl(bexc, c);
+    const int64_t p0_c = __shfl(p0, c);
+    int s = 0, len = 0;
+    double bv = 0.0;
+    if (e < totalB) {
+      const int64_t p = p0_c + (e - ex_c);
+      const int2 m = cmap[irB[p]];
+      s = m.x;
+      len = m.y;
+      bv = valB[p];
+    }
+    const int pincl = wave_incl_scan(len);
+    const int ptot = wave_last(pincl);
+    if (ptot == 0) continue;
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) {
+      if (pbase + ptot <= j * WAVE || pbase >= (j + 1) * WAVE) continue;  // uniform
+      // element j * 64 + lane takes product q of this round: its entry is the
+      // first lane whose inclusive product count exceeds q
+      const int q = j * WAVE + lane - pbase;
+      int lo = 0, hi = WAVE - 1;
+#pragma unroll
+      for (int it = 0; it < 6; ++it) {
+        const int mid = (lo + hi) >> 1;
+        const int v = __shfl(pincl, mid);
+        if (v > q) hi = mid; else lo = mid + 1;
+      }
+      const int o = lo;
+      const int o_s = __shfl(s, o), o_ex = __shfl(pincl - len, o), o_c = __shfl(c, o);
+      const double o_bv = __shfl(bv, o);
+      if (q >= 0 && q < ptot) {
+        const int a = o_s + (q - o_ex);
+        key[j] = (o_c << SH) | irA[a];
+        val[j] = Sem<SR>::mul(valA[a], o_bv);
+      }
+    }
+    pbase += ptot;
+  }
+  if constexpr (NPL == 1) {
+    wave_bitonic_sort_kv(key[0], val[0], lane);
+  } else {
+    wave_bitonic_sort_kvn<NPL>(key, val, lane);
+  }
+  // combine equal keys: segmented inclusive scan per register (keys are sorted,
+  // so a lane d below with the same key means every lane in between has it
+  // too), then the run that continues from the previous register's top lane
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const int ok = __shfl_up(key[j], d);
+      const double ov = __shfl_up(val[j], d);
+      if (lane >= d && ok == key[j]) val[j] = Sem<SR>::add(ov, val[j]);
+    }
+    if (j > 0) {
+      const int pk = __builtin_amdgcn_readlane(key[j - 1], WAVE - 1);
+      const double pv = __shfl(val[j - 1], WAVE - 1);
+      if (key[j] == pk) val[j] = Sem<SR>::add(pv, val[j]);
+    }
+  }
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int pos[NPL], mycount = 0;
+  bool tail[NPL];
+  int cj[NPL];
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    int nk = __shfl_down(key[j], 1);
+    if (j + 1 < NPL) {
+      const int f = __builtin_amdgcn_readlane(key[j + 1 < NPL ? j + 1 : j], 0);
+      if (lane == WAVE - 1) nk = f;
+    }
+    tail[j] = key[j] != EMPTY_KEY && ((lane == WAVE - 1 && j == NPL - 1) || nk != key[j]);
+    cj[j] = key[j] != EMPTY_KEY ? key[j] >> SH : 0;
+    pos[j] = 0;
+  }
+#pragma unroll
+  for (int cc = 0; cc < CPW; ++cc) {
+    int before = 0;  // tails of column cc in the registers below
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) {
+      const unsigned long long m = __ballot(tail[j] && cj[j] == cc);
+      if (cj[j] == cc) pos[j] = before + __popcll(m & lt);
+      before += __popcll(m);
+    }
+    if (lane == cc) mycount = before;
+  }
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    if (tail[j]) {
+      const int64_t o = (idx0 + cj[j]) * (int64_t)fmax + pos[j];
+      tir[o] = key[j] & (int)((1u << SH) - 1u);
+      tval[o] = val[j];
+    }
+  }
+  if (col >= 0) {
+    cnt[col] = mycount;
+    tslot[col] = slot_base + (idx0 + lane) * (int64_t)fmax;
+  }
+}
+
+// the fused columns' temporary slots -> C, in COLUMN order (tslot[col] >= 0:
+// the column's slot; -1: not fused): a wave's threads take consecutive
+// columns, so C's entries are written in order (a pass over the bins in their
+// perm order scattered its stores over C and gathered perm / cnt / colptr)
+constexpr int COPY_TPC = 4;  // threads per column
+__global__ void k_copy_fused(int64_t nz, const int64_t* __restrict__ tslot, const int32_t* __restrict__ cnt,
                              const int64_t* __restrict__ colptr, const int32_t* __restrict__ tir,
                              const double* __restrict__ tval, int32_t* __restrict__ out_ir,
                              double* __restrict__ out_val) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t idx = t / FMAX;
-  const int e = (int)(t % FMAX);
-  if (idx >= n) return;
-  const int col = perm[idx];
-  if (e < cnt[col]) {
-    st_stream(&out_ir[colptr[col] + e], tir[idx * FMAX + e]);
-    st_stream(&out_val[colptr[col] + e], tval[idx * FMAX + e]);
+  const int64_t col = t / COPY_TPC;
+  if (col >= nz) return;
+  const int64_t src = tslot[col];
+  if (src < 0) return;
+  const int c = cnt[col];
+  const int64_t o = colptr[col];
+  for (int e = (int)(t % COPY_TPC); e < c; e += COPY_TPC) {
+    out_ir[o + e] = tir[src + e];
+    out_val[o + e] = tval[src + e];
   }
 }
 
@@ -1749,7 +2102,10 @@ static void set_lds(K kernel, size_t bytes) {
 // bins of the symbolic phase (key = flops)
 //  0: F == 0 | 1: <=32 wave T64 | 2: <=128 wave T256 | 3: <=512 wave T1024 |
 //  4: <=1024 block T2048 | 5: <=2048 block T4096 | 6: <=4096 block T8192 | 7: big
-static const int64_t kSymThr[] = {0, 32, 128, 512, 1024, 2048, 4096};
+// symbolic bins: 1-8 (flops <= 2 ... 256) expand-sort-compress waves of 32 ... 1
+// columns (symbolic and numeric in one pass), 9 (<= 512) wave hash, 10-12 block hash
+static const int64_t kSymThr[] = {0, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096};
+constexpr int SYM_FUSED_LAST = 8;
 // columns with more flops than this take the bitmap+rank slab path (runtime
 // override: CBG_BIG_FLOPS); it must stay <= 4096 so that every other column's
 // nnz fits the largest numeric hash bin
@@ -1783,6 +2139,40 @@ static void launch_fused(const int32_t* perm, int n, const cbg_tile& B, const in
   set_lds(k_fused_wave<LOGT, SR, FMAX>, lds);
   hipLaunchKernelGGL((k_fused_wave<LOGT, SR, FMAX>), dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, B.val,
                      cmap, A.ir, A.val, cnt, tir, tval);
+}
+// expand-sort-compress bin b (flops <= fmax = 64 >> (b - 1)... as CPW = 64 / fmax
+// columns per wave; one column per wave when A's rows leave no room for the
+// column bits of the sort key)
+template <int CPW, int NPL, int SR>
+static void launch_esc1(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
+                        const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((k_esc_wave<CPW, NPL, SR>), dim3(nblk((n + CPW - 1) / CPW, 4)), dim3(256), 0, s, perm, n, fmax,
+                     B.cp, B.ir, B.val, cmap, A.ir, A.val, cnt, tir + base, tval + base, base, tslot);
+}
+// expand-sort-compress bin of flops <= fmax: CPW = 64 * NPL / fmax columns per
+// wave (one column per wave when A's rows leave no room for the column bits of
+// the sort key); fmax 128 / 256 sort 2 / 4 products per lane
+template <int SR>
+static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
+                       const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  if (fmax > 2 * WAVE) return launch_esc1<1, 4, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+  if (fmax > WAVE) return launch_esc1<1, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+  int cpw = 1;
+  while (cpw * fmax * 2 <= WAVE && cpw < 32) cpw <<= 1;  // CPW * fmax <= 64
+  int logc = 0;
+  while ((1 << logc) < cpw) ++logc;
+  if (A.m >= (1LL << (31 - logc))) cpw = 1;  // key = c << (31 - logc) | row must stay below EMPTY_KEY
+  switch (cpw) {
+    case 32: launch_esc1<32, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    case 16: launch_esc1<16, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    case 8: launch_esc1<8, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    case 4: launch_esc1<4, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    case 2: launch_esc1<2, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    default: launch_esc1<1, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+  }
 }
 template <int LOGT, int BS>
 static void launch_sym_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
@@ -1987,6 +2377,7 @@ static double bitmap_budget_bytes() {
 
 struct Binned {
   std::vector<int> count, offset;
+  std::vector<unsigned long long> flops;  // per bin
   DBuf<int32_t> perm;
 };
 
@@ -1999,18 +2390,29 @@ struct BinPending {
   DBuf<uint8_t> bin;
   DBuf<int> hist;
   std::vector<int> h;
+  std::vector<unsigned long long> hf;  // flops per bin
+  unsigned long long big_entries = 0;
 };
+// cpB/big_bin (mode 0): also count the B entries of the bins >= big_bin into bp.big_entries
 static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
-                         int nthr, int64_t big, BinPending& bp, hipStream_t s, int64_t fused_max = 0) {
+                         int nthr, int64_t big, BinPending& bp, hipStream_t s, int64_t fused_max = 0,
+                         const int64_t* cpB = nullptr, int big_bin = MAXBINS) {
   bp.bt.nb = nthr + 1;
   for (int i = 0; i < nthr; ++i) bp.bt.t[i] = thr[i];
   bp.bin.reset(n);
-  bp.hist.reset(2 * MAXBINS);
-  CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * 2 * MAXBINS, s));
-  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt, bp.bin.p,
-                     bp.hist.p, fused_max);
+  // counts | offsets | big entries (u64) | flops per bin (u64)
+  bp.hist.reset(2 * MAXBINS + 2 + 2 * MAXBINS);
+  CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * (4 * MAXBINS + 2), s));
+  unsigned long long* be = cpB ? reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS) : nullptr;
+  unsigned long long* bf = reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS + 2);
+  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt,
+                     bp.bin.p, bp.hist.p, fused_max, cpB, big_bin, be, bf);
   bp.h.assign(MAXBINS, 0);
   CBG_HIP(hipMemcpyAsync(bp.h.data(), bp.hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
+  bp.big_entries = 0;
+  if (be) CBG_HIP(hipMemcpyAsync(&bp.big_entries, be, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  bp.hf.assign(MAXBINS, 0);
+  CBG_HIP(hipMemcpyAsync(bp.hf.data(), bf, sizeof(unsigned long long) * MAXBINS, hipMemcpyDeviceToHost, s));
 }
 static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, DeferredFree& df) {
   const int nb = bp.bt.nb;
@@ -2020,9 +2422,10 @@ static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, D
     out.count[b] = bp.h[b];
     out.offset[b + 1] = out.offset[b] + bp.h[b];
   }
+  out.flops = bp.hf;
   CBG_HIP(hipMemcpyAsync(bp.hist.p + MAXBINS, out.offset.data(), sizeof(int) * nb, hipMemcpyHostToDevice, s));
   out.perm.reset(n);
-  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256)), dim3(256), 0, s, n, bp.bin.p, nb, bp.hist.p + MAXBINS,
+  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, bp.bin.p, nb, bp.hist.p + MAXBINS,
                      out.perm.p);
   df.take(bp.bin);  // released after the multiply's final synchronization
   df.take(bp.hist);
@@ -2043,23 +2446,45 @@ static bool block_bins_persistent() {
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* valAf, const cbg_tile& B,
-                             const int2* cmap, const int64_t* colptr, cbg_tile& C, hipStream_t s, DeferredFree& df) {
+                             const int2* cmap, const int64_t* colptr, cbg_tile& C, const hipStream_t* sb,
+                             DeferredFree& df) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
-  launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, s);
-  launch_num_wave<7, SR>(at(2), nb.count[2], B, cmap, A, colptr, C, s);
-  launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, s);
-  launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, s);
+  launch_num_wave<6, SR>(at(1), nb.count[1], B, cmap, A, colptr, C, sb[1]);
+  launch_num_wave<7, SR>(at(2), nb.count[2], B, cmap, A, colptr, C, sb[2]);
+  launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, sb[3]);
+  launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, sb[4]);
   if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, s, df);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, s, df);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, s, df);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, s, df);
+    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, sb[5], df);
+    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, sb[6], df);
+    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, sb[7], df);
+    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, sb[8], df);
   } else {
-    launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, s);
-    launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, s);
-    launch_num_block<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, s);
-    launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, s);
+    launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, sb[5]);
+    launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, sb[6]);
+    launch_num_block<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, sb[7]);
+    launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, sb[8]);
+  }
+}
+
+// Stream of each small-column bin: the big columns run on the main stream,
+// the small bins on the side stream concurrently -- unless the big columns
+// carry less work than the small ones (GalerkinNew: 6 % of the flops), when
+// bins from the largest down go to whichever stream has less work so far, so
+// that both finish together.  Work = flops x the bin's relative cost.
+static void balance_bins(const std::vector<unsigned long long>& fl, int first, int last, double main_work,
+                         double side_work, const double* cost, hipStream_t main, hipStream_t side,
+                         hipStream_t* out) {
+  static const int bal = getenv("CBG_BALANCE") ? atoi(getenv("CBG_BALANCE")) : 0;  // 1: GalerkinNew 10.0 -> 9.9-10.2 ms (the streams share one saturated GPU): off
+  for (int b = last; b >= first; --b) {
+    const double w = (double)fl[b] * (cost ? cost[b] : 1.0);
+    if (!bal || side == main || side_work <= main_work) {
+      out[b] = side;
+      side_work += w;
+    } else {
+      out[b] = main;
+      main_work += w;
+    }
   }
 }
 
@@ -2078,16 +2503,58 @@ struct APrep {
 // exactly (NaN and values outside f32's range or precision do not).  When they
 // all do, the slab kernels read 4 B per product instead of 8 and widen them:
 // the products and sums are the f64 ones, bit for bit.  CBG_AF32=0 disables.
+// (stops early once some value is inexact: the copy is then not used --
+// GalerkinNew's A = L + D carries random diagonal values, and each of its
+// products checked all 68 M values for nothing: 0.21 ms)
 __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __restrict__ f, int* __restrict__ inexact) {
-  bool bad = false;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double x = v[i];
-    const float y = (float)x;
-    f[i] = y;
-    bad |= !((double)y == x);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  while (i < n) {
+    if (*reinterpret_cast<volatile int*>(inexact)) return;
+    bool bad = false;
+#pragma unroll
+    for (int u = 0; u < 8; ++u, i += stride) {
+      if (i < n) {
+        const double x = v[i];
+        const float y = (float)x;
+        f[i] = y;
+        bad |= !((double)y == x);
+      }
+    }
+    // one store per wave, and none once the flag is up: a million threads
+    // storing to one address serialized at L2 (0.3 ms)
+    const unsigned long long any = __ballot(bad);
+    if (any) {
+      if (lane_id() == __ffsll((long long)any) - 1 && !*reinterpret_cast<volatile int*>(inexact))
+        *reinterpret_cast<volatile int*>(inexact) = 1;
+      return;
+    }
   }
-  if (bad) *inexact = 1;
 }
+// flops[0, nz) per B column and their total in flops[nz] (B.nnz > 0)
+static void launch_flops(const cbg_tile& B, const int2* cmap, int64_t* flops, hipStream_t s, DeferredFree& df) {
+  const int64_t nz = B.nzc;
+  static const bool classic = getenv("CBG_FLOPS_CLASSIC") && atoi(getenv("CBG_FLOPS_CLASSIC"));
+  if (classic) {  // a lane group per column + hub tail (before round 3)
+    CBG_HIP(hipMemsetAsync(flops + nz, 0, sizeof(int64_t), s));
+    DBuf<int> longq(nz + 1);  // count | queued columns
+    CBG_HIP(hipMemsetAsync(longq.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap, flops, longq.p);
+    hipLaunchKernelGGL(k_flops_tail, dim3((unsigned)std::min<int64_t>(nz, 1024)), dim3(256), 0, s, B.cp, B.ir, cmap,
+                       nz, flops, longq.p);
+    df.take(longq);
+    return;
+  }
+  const int64_t nb = (B.nnz + FSEG_E - 1) / FSEG_E;
+  DBuf<unsigned long long> part(nb);
+  CBG_HIP(hipMemsetAsync(flops, 0, sizeof(int64_t) * nz, s));
+  hipLaunchKernelGGL(k_flops_seg, dim3((unsigned)nb), dim3(FSEG_T), 0, s, nz, B.nnz, B.cp, B.ir, cmap,
+                     reinterpret_cast<unsigned long long*>(flops), part.p);
+  hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, s, part.p, nb,
+                     reinterpret_cast<unsigned long long*>(flops + nz));
+  df.take(part);
+}
+
 static bool af32_enabled() {
   static const char* e = getenv("CBG_AF32");
   return !(e && !strcmp(e, "0"));
@@ -2209,16 +2676,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
 
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
-  CBG_HIP(hipMemsetAsync(flops.p + nz, 0, sizeof(int64_t), s));
-  {
-    DBuf<int> longq(nz + 1);  // count | queued columns
-    CBG_HIP(hipMemsetAsync(longq.p, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap.p, flops.p,
-                       longq.p);
-    hipLaunchKernelGGL(k_flops_tail, dim3((unsigned)std::min<int64_t>(nz, 1024)), dim3(256), 0, s, B.cp, B.ir, cmap.p,
-                       nz, flops.p, longq.p);
-    df.take(longq);
-  }
+  launch_flops(B, cmap.p, flops.p, s, df);
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
@@ -2232,9 +2690,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // group size 2^GROUP_LOG_MAX .. 1 (columns with F * g / R <= GROUP_PRODUCTS
   // expected products per group; CBG_GROUPS=0 keeps every pair on its own)
   BigPlan bp;
+  int64_t big_entries = 0;  // B entries of the big columns (read back with sync 1)
   bp.plog = pick_panel_log(A.m);
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
-  constexpr int NSMALL = 7, NGCLS = GROUP_LOG_MAX + 1;
+  constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1;
+  static_assert(NSMALL + NGCLS <= MAXBINS, "bins");
   {
     static const char* eg = getenv("CBG_GROUPS");
     static const char* ep = getenv("CBG_GROUP_PRODUCTS");
@@ -2249,9 +2709,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       thr[NSMALL + c] = (groups && g <= bp.R && g <= (1LL << glmax)) ? gp * bp.R / g : -1;
     }
     BinPending sp;
-    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sp, s);
+    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sp, s, 0, B.cp, NSMALL);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
     bin_scatter(nz, sp, sb, s, df);
+    big_entries = (int64_t)sp.big_entries;
   }
   // small-column symbolic bins on the side stream, big columns on the main one
   // (bins 1-2 fused with their numeric unless CBG_FUSE_SMALL=0)
@@ -2259,31 +2720,53 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const bool fused = fuse_small;
   DBuf<int32_t> fused_ir;
   DBuf<double> fused_val;
+  DBuf<int64_t> fused_slot;  // temporary slot of each fused column (-1: none)
+  size_t fused_off[SYM_FUSED_LAST + 2] = {};  // temporary slots of the fused bins 1..SYM_FUSED_LAST
+  // slot width of fused bin b: its flops bound (big >= 64 never clips bins 1..6,
+  // and a clipped bin 7 / 8 holds columns of <= big flops)
+  auto fmax_of = [&](int b) { return (int)kSymThr[b]; };
+  if (fused) {
+    fused_slot.reset(nz);
+    CBG_HIP(hipMemsetAsync(fused_slot.p, 0xff, sizeof(int64_t) * nz, s));  // -1: not fused (before the fork)
+  }
   fork(s);
+  // streams of the small symbolic bins (balance_bins; the fused bins also do
+  // their numeric work: cost 2 per flop)
+  hipStream_t symst[NSMALL];
+  {
+    double main_w = 0.0;
+    for (int b = NSMALL; b < NSMALL + NGCLS; ++b) main_w += (double)sb.flops[b];
+    double cost[NSMALL];
+    for (int b = 0; b < NSMALL; ++b) cost[b] = (fused && b >= 1 && b <= SYM_FUSED_LAST) ? 2.0 : 1.0;
+    symst[0] = ssym;
+    balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, ssym, symst);
+  }
   {
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
     if (fused) {
-      // bins 1-2 (flops <= 32, <= 128): symbolic and numeric in one pass into fused_ir/val
-      fused_ir.reset((size_t)sb.count[1] * 32 + (size_t)sb.count[2] * 128 + 1);
-      fused_val.reset((size_t)sb.count[1] * 32 + (size_t)sb.count[2] * 128 + 1);
-      if (semiring == CBG_MIN_PLUS) {
-        launch_fused<6, 1, 32>(at(1), sb.count[1], B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p, ssym);
-        launch_fused<8, 1, 128>(at(2), sb.count[2], B, cmap.p, A, cnt.p, fused_ir.p + (size_t)sb.count[1] * 32,
-                                fused_val.p + (size_t)sb.count[1] * 32, ssym);
-      } else {
-        launch_fused<6, 0, 32>(at(1), sb.count[1], B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p, ssym);
-        launch_fused<8, 0, 128>(at(2), sb.count[2], B, cmap.p, A, cnt.p, fused_ir.p + (size_t)sb.count[1] * 32,
-                                fused_val.p + (size_t)sb.count[1] * 32, ssym);
+      // bins 1..8 (flops <= 256): symbolic and numeric in one pass into fused_ir/val
+      for (int b = 1; b <= SYM_FUSED_LAST; ++b)
+        fused_off[b + 1] = fused_off[b] + (size_t)sb.count[b] * (size_t)fmax_of(b);
+      fused_ir.reset(fused_off[SYM_FUSED_LAST + 1] + 1);
+      fused_val.reset(fused_off[SYM_FUSED_LAST + 1] + 1);
+      for (int b = 1; b <= SYM_FUSED_LAST; ++b) {
+        if (semiring == CBG_MIN_PLUS)
+          launch_esc<1>(at(b), sb.count[b], fmax_of(b), B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p,
+                        (int64_t)fused_off[b], fused_slot.p, symst[b]);
+        else
+          launch_esc<0>(at(b), sb.count[b], fmax_of(b), B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p,
+                        (int64_t)fused_off[b], fused_slot.p, symst[b]);
       }
     } else {
-      launch_sym_wave<6>(at(1), sb.count[1], B, cmap.p, A, cnt.p, ssym);
-      launch_sym_wave<8>(at(2), sb.count[2], B, cmap.p, A, cnt.p, ssym);
+      for (int b = 1; b <= 5; ++b) launch_sym_wave<6>(at(b), sb.count[b], B, cmap.p, A, cnt.p, symst[b]);
+      for (int b = 6; b <= 7; ++b) launch_sym_wave<8>(at(b), sb.count[b], B, cmap.p, A, cnt.p, symst[b]);
+      launch_sym_wave<10>(at(8), sb.count[8], B, cmap.p, A, cnt.p, symst[8]);
     }
-    launch_sym_wave<10>(at(3), sb.count[3], B, cmap.p, A, cnt.p, ssym);
-    launch_sym_block<11, 256>(at(4), sb.count[4], B, cmap.p, A, cnt.p, ssym);
-    launch_sym_block<12, 256>(at(5), sb.count[5], B, cmap.p, A, cnt.p, ssym);
-    launch_sym_block<13, 512>(at(6), sb.count[6], B, cmap.p, A, cnt.p, ssym);
+    launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
+    launch_sym_block<11, 256>(at(10), sb.count[10], B, cmap.p, A, cnt.p, symst[10]);
+    launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, A, cnt.p, symst[11]);
+    launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, A, cnt.p, symst[12]);
   }
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
@@ -2305,8 +2788,19 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
+    static const int pm_entries = getenv("CBG_PMAP_ENTRIES") ? atoi(getenv("CBG_PMAP_ENTRIES")) : 64;
     if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
       bp.cmapP = ap.cmapP.p;
+    } else if (bp.R > 1 && pm_entries > 0 && big_entries * pm_entries < A.nzc) {
+      // few big-column entries (GalerkinNew's A*T: ~10^3 of A's 4 M columns;
+      // not the phase plan's sample of scale 22, 1/10 of them, whose hub
+      // references would each search their long A column again):
+      // map only the A columns they reference, without the memset of the
+      // R x n map; this B's own map, never cached for other pieces / phases
+      bp.cmapP_own.reset((size_t)bp.R * (A.n + 1));
+      hipLaunchKernelGGL(k_colmap_panels_entries, dim3(nblk((int64_t)nbig * WAVE, 256)), dim3(256), 0, s,
+                         bp.perm_big, nbig, B.cp, B.ir, cmap.p, A.ir, bp.plog, bp.R, A.n + 1, bp.cmapP_own.p);
+      bp.cmapP = bp.cmapP_own.p;
     } else {
       DBuf<int2>& cp = ap.active ? ap.cmapP : bp.cmapP_own;
       cp.reset((size_t)bp.R * (A.n + 1));
@@ -2381,7 +2875,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   BinPending npend;
-  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[2] : 0);
+  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[SYM_FUSED_LAST] : 0);
   // compaction of C's columns (SpDCCols(SpTuples): nonempty columns only)
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
@@ -2466,18 +2960,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bin_scatter(nz, npend, nbn, s, df);
   // small-column bins on the side stream, big-column slabs on the main one
   fork(s);
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, snum, df);
-  else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, snum, df);
-  if (fused) {
-    const int32_t* P = sb.perm.p;
-    if (sb.count[1] > 0)
-      hipLaunchKernelGGL(k_copy_fused<32>, dim3(nblk((int64_t)sb.count[1] * 32, 256)), dim3(256), 0, snum,
-                         P + sb.offset[1], sb.count[1], cnt.p, colptr.p, fused_ir.p, fused_val.p, C.ir, C.val);
-    if (sb.count[2] > 0)
-      hipLaunchKernelGGL(k_copy_fused<128>, dim3(nblk((int64_t)sb.count[2] * 128, 256)), dim3(256), 0, snum,
-                         P + sb.offset[2], sb.count[2], cnt.p, colptr.p, fused_ir.p + (size_t)sb.count[1] * 32,
-                         fused_val.p + (size_t)sb.count[1] * 32, C.ir, C.val);
+  hipStream_t numst[10];
+  {
+    // the slabs of the big columns on the main stream; the fused bins' copies on
+    // the side one (about a quarter of a product's cost per entry)
+    double fused_w = 0.0;
+    if (fused)
+      for (int b = 1; b <= SYM_FUSED_LAST; ++b) fused_w += 0.25 * (double)sb.flops[b];
+    numst[0] = numst[9] = snum;
+    balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst);
   }
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
+  else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
+  if (fused && fused_off[SYM_FUSED_LAST + 1] > 0)
+    hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz * COPY_TPC, 256)), dim3(256), 0, snum, nz, fused_slot.p, cnt.p,
+                       colptr.p, fused_ir.p, fused_val.p, C.ir, C.val);
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);

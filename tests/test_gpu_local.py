@@ -95,6 +95,61 @@ def test_random_fp_vs_oracle(cbg, seed):
     assert_tiles_equal(Cm, oracle_local(Ah, Bh, "minplus"))
 
 
+def _sparse_cols(rng, m, lens, dup_rows=None):
+    """DCSC with column j holding lens[j] distinct sorted random rows (0 = empty column dropped)"""
+    cols, rows = [], []
+    for j, L in enumerate(lens):
+        if L == 0:
+            continue
+        r = np.sort(rng.choice(m if dup_rows is None else dup_rows, L, replace=False))
+        cols.append(np.full(L, j))
+        rows.append(r)
+    cols = np.concatenate(cols)
+    rows = np.concatenate(rows)
+    jc, start = np.unique(cols, return_index=True)
+    return dict(m=m, n=len(lens), cp=np.append(start, len(rows)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=rows.astype(np.int32), val=rng.uniform(-1.0, 1.0, len(rows)))
+
+
+@pytest.mark.parametrize("m", [5000, (1 << 27) + 5])
+def test_small_column_esc(cbg, m):
+    # columns of <= 256 products run through the expand-sort-compress waves
+    # (k_esc_wave: 32 ... 1 columns per wave, 1, 2 or 4 products per lane); rows
+    # concentrated on few values force duplicate keys inside a wave, B columns
+    # of many entries on empty A columns force several staging rounds, and
+    # m >= 2^27 leaves no room for column bits in the sort key (CPW = 1)
+    rng = np.random.default_rng(5)
+    k = 400
+    hot = np.arange(0, m, max(1, m // 40))[:40]      # 40 row values: many duplicates
+    lensA = rng.integers(0, 9, k)
+    lensA[::7] = 0                                      # empty A columns
+    Ah = _sparse_cols(rng, m, lensA, dup_rows=hot)
+    Ah["n"] = k
+    nB = 3000
+    ir, cp = [], [0]
+    for j in range(nB):
+        target = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 100, 128, 160, 200, 256]))
+        ks, f = [], 0
+        for kk in rng.permutation(k):
+            L = int(lensA[kk])
+            if f + L > target:
+                continue
+            ks.append(kk)
+            f += L
+            if f == target or len(ks) > 90:
+                break
+        ks = sorted(ks) if ks else [int(np.argmax(lensA == 0))]
+        ir.extend(ks)
+        cp.append(len(ir))
+    Bh = dict(m=k, n=nB, cp=np.array(cp, np.int64), jc=np.arange(nB, dtype=np.int32),
+              ir=np.array(ir, np.int32), val=rng.uniform(-1.0, 1.0, len(ir)))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh)).to_host()
+    bound = oracle_local(abs_tile(Ah), abs_tile(Bh))["val"]
+    assert_tiles_equal(C, oracle_local(Ah, Bh), rtol=RTOL, bound=bound)
+    Cm = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), "minplus").to_host()
+    assert_tiles_equal(Cm, oracle_local(Ah, Bh, "minplus"))
+
+
 def test_big_columns_tall_matrix(cbg):
     # m > 2^20 rows exercises multi-pass bitmaps and hash-mode slabs
     rng = np.random.default_rng(7)
