@@ -198,6 +198,16 @@ struct DeferredFree;
 void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df = nullptr);
 void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipStream_t s, DeferredFree* df = nullptr);
 
+// thin big columns of the local multiply (cbg_thin.hip): the n columns perm[]
+// (fthin products in all) expanded, sorted and reduced into tir/tval[base ...];
+// cnt[col] = their nnz, tslot[col] = their first temporary position
+// (E = their B entries); thin_copy moves them to C after the column scan
+void thin_columns(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
+                  const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval,
+                  int64_t base, hipStream_t s, DeferredFree& df);
+void thin_copy(const int32_t* perm, int n, const int64_t* tslot, const int32_t* cnt, const int64_t* colptr,
+               const int32_t* tir, const double* tval, int32_t* out_ir, double* out_val, hipStream_t s);
+
 // multiway merge of column-sorted partial tiles (cbg_merge.hip)
 // int64 entry counts: column chunks of < 2^30 stacked entries (CBG_MERGE_CHUNK
 // overrides) each run as one product into an EntryArena

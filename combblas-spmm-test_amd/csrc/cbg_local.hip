@@ -247,23 +247,28 @@ struct BinThr {
 // per-block histogram atomics -- a few hundred blocks on 16 addresses -- do
 // not serialize (one block per 256 columns: 80 us for 2 M columns).
 constexpr int BIN_ITEMS = 16;
-// big_entries (mode 0, optional): B entries of the columns in bins >= big_bin
+// big_entries (mode 0, optional): B entries of the columns in bins >= big_bin,
+// [0] the big ones, [1] the thin ones
+// thin_R > 0: big columns with flops * THIN_RATIO < B entries * thin_R go to
+// thin_bin (mode 0) / are skipped like the fused ones (mode 1)
+constexpr int64_t THIN_RATIO = 4;
 __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __restrict__ flops,
                                                   const int32_t* __restrict__ cnt, int mode, int64_t big, BinThr thr,
                                                   uint8_t* __restrict__ bin, int* __restrict__ hist,
                                                   int64_t fused_max, const int64_t* __restrict__ cpB, int big_bin,
                                                   unsigned long long* __restrict__ big_entries,
-                                                  unsigned long long* __restrict__ bin_flops) {
+                                                  unsigned long long* __restrict__ bin_flops, int thin_R,
+                                                  int thin_bin) {
   __shared__ int lh[MAXBINS];
   __shared__ unsigned long long lf[MAXBINS];
-  __shared__ unsigned long long lbe;
+  __shared__ unsigned long long lbe, lbt;
   if (threadIdx.x < MAXBINS) {
     lh[threadIdx.x] = 0;
     lf[threadIdx.x] = 0;
   }
-  if (threadIdx.x == 0) lbe = 0;
+  if (threadIdx.x == 0) lbe = lbt = 0;
   __syncthreads();
-  unsigned long long be = 0;
+  unsigned long long be = 0, bt = 0;
   const int64_t i0 = blockIdx.x * (int64_t)(256 * BIN_ITEMS) + threadIdx.x;
 #pragma unroll 4
   for (int j = 0; j < BIN_ITEMS; ++j) {
@@ -271,23 +276,29 @@ __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __re
     if (i < n) {
       const int64_t f = flops[i];
       int64_t key = f;
+      // thin big columns (cbg_thin.hip): few products per B entry, so the R
+      // (column, panel) pairs would each stage the whole column for little
+      const bool thin = thin_R > 0 && f > big && f * THIN_RATIO < (cpB[i + 1] - cpB[i]) * (int64_t)thin_R;
       // numeric bins: big columns last; columns computed by the fused small-column
-      // pass (0 < flops <= fused_max) in bin 0, which the numeric skips
-      if (mode == 1) key = (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
+      // pass (0 < flops <= fused_max) or the thin pass in bin 0, which the numeric skips
+      if (mode == 1) key = thin ? 0 : (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
       int b = thr.nb - 1;
       for (int q = 0; q < thr.nb - 1; ++q)
         if (key <= thr.t[q]) { b = q; break; }
+      if (mode == 0 && thin) b = thin_bin;
       bin[i] = (uint8_t)b;
       atomicAdd(&lh[b], 1);
       if (f > 0) atomicAdd(&lf[b], (unsigned long long)f);
-      if (big_entries && b >= big_bin) be += (unsigned long long)(cpB[i + 1] - cpB[i]);
+      if (big_entries && b >= big_bin) (thin ? bt : be) += (unsigned long long)(cpB[i + 1] - cpB[i]);
     }
   }
   if (big_entries && be) atomicAdd(&lbe, be);
+  if (big_entries && bt) atomicAdd(&lbt, bt);
   __syncthreads();
   if (threadIdx.x < thr.nb && lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
   if (threadIdx.x < thr.nb && lf[threadIdx.x]) atomicAdd(&bin_flops[threadIdx.x], lf[threadIdx.x]);
   if (big_entries && threadIdx.x == 0 && lbe) atomicAdd(big_entries, lbe);
+  if (big_entries && threadIdx.x == 0 && lbt) atomicAdd(big_entries + 1, lbt);
 }
 
 __global__ __launch_bounds__(256) void k_bin_scatter(int64_t n, const uint8_t* __restrict__ bin, int nb,
@@ -1498,12 +1509,12 @@ constexpr int COPY_TPC = 4;  // threads per column
 __global__ void k_copy_fused(int64_t nz, const int64_t* __restrict__ tslot, const int32_t* __restrict__ cnt,
                              const int64_t* __restrict__ colptr, const int32_t* __restrict__ tir,
                              const double* __restrict__ tval, int32_t* __restrict__ out_ir,
-                             double* __restrict__ out_val) {
+                             double* __restrict__ out_val, int64_t thin_base) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t col = t / COPY_TPC;
   if (col >= nz) return;
   const int64_t src = tslot[col];
-  if (src < 0) return;
+  if (src < 0 || src >= thin_base) return;  // not fused / a thin column (thin_copy)
   const int c = cnt[col];
   const int64_t o = colptr[col];
   for (int e = (int)(t % COPY_TPC); e < c; e += COPY_TPC) {
@@ -2391,26 +2402,26 @@ struct BinPending {
   DBuf<int> hist;
   std::vector<int> h;
   std::vector<unsigned long long> hf;  // flops per bin
-  unsigned long long big_entries = 0;
+  unsigned long long big_entries[2] = {0, 0};  // B entries of the big / thin columns
 };
 // cpB/big_bin (mode 0): also count the B entries of the bins >= big_bin into bp.big_entries
 static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
                          int nthr, int64_t big, BinPending& bp, hipStream_t s, int64_t fused_max = 0,
-                         const int64_t* cpB = nullptr, int big_bin = MAXBINS) {
+                         const int64_t* cpB = nullptr, int big_bin = MAXBINS, int thin_R = 0, int thin_bin = 0) {
   bp.bt.nb = nthr + 1;
   for (int i = 0; i < nthr; ++i) bp.bt.t[i] = thr[i];
   bp.bin.reset(n);
-  // counts | offsets | big entries (u64) | flops per bin (u64)
-  bp.hist.reset(2 * MAXBINS + 2 + 2 * MAXBINS);
-  CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * (4 * MAXBINS + 2), s));
-  unsigned long long* be = cpB ? reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS) : nullptr;
-  unsigned long long* bf = reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS + 2);
+  // counts | offsets | big, thin entries (u64) | flops per bin (u64)
+  bp.hist.reset(2 * MAXBINS + 4 + 2 * MAXBINS);
+  CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * (4 * MAXBINS + 4), s));
+  unsigned long long* be = (cpB && mode == 0) ? reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS) : nullptr;
+  unsigned long long* bf = reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS + 4);
   hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt,
-                     bp.bin.p, bp.hist.p, fused_max, cpB, big_bin, be, bf);
+                     bp.bin.p, bp.hist.p, fused_max, cpB, big_bin, be, bf, thin_R, thin_bin);
   bp.h.assign(MAXBINS, 0);
   CBG_HIP(hipMemcpyAsync(bp.h.data(), bp.hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
-  bp.big_entries = 0;
-  if (be) CBG_HIP(hipMemcpyAsync(&bp.big_entries, be, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  bp.big_entries[0] = bp.big_entries[1] = 0;
+  if (be) CBG_HIP(hipMemcpyAsync(bp.big_entries, be, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   bp.hf.assign(MAXBINS, 0);
   CBG_HIP(hipMemcpyAsync(bp.hf.data(), bf, sizeof(unsigned long long) * MAXBINS, hipMemcpyDeviceToHost, s));
 }
@@ -2690,18 +2701,24 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // group size 2^GROUP_LOG_MAX .. 1 (columns with F * g / R <= GROUP_PRODUCTS
   // expected products per group; CBG_GROUPS=0 keeps every pair on its own)
   BigPlan bp;
-  int64_t big_entries = 0;  // B entries of the big columns (read back with sync 1)
+  int64_t big_entries = 0, thin_entries = 0;  // B entries of the big / thin columns (read back with sync 1)
+  // small columns' symbolic and numeric in one pass (bins 1..SYM_FUSED_LAST), unless CBG_FUSE_SMALL=0
+  static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
+  const bool fused = fuse_small;
   bp.plog = pick_panel_log(A.m);
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
-  constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1;
-  static_assert(NSMALL + NGCLS <= MAXBINS, "bins");
+  constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1, THIN_BIN = NSMALL + NGCLS;
+  static_assert(THIN_BIN < MAXBINS, "bins");
+  constexpr int64_t THIN_MAX_FLOPS = 1LL << 27;  // int item counts of the sort; ~4 GB of temporaries
+  int thin_R = 0;
   {
     static const char* eg = getenv("CBG_GROUPS");
     static const char* ep = getenv("CBG_GROUP_PRODUCTS");
     const bool groups = !(eg && !strcmp(eg, "0"));
     const int64_t gp = ep ? atoll(ep) : GROUP_PRODUCTS;
-    int64_t thr[NSMALL + NGCLS - 1];
+    int64_t thr[NSMALL + NGCLS];
     for (int i = 0; i < NSMALL; ++i) thr[i] = std::min(kSymThr[i], big);
+    thr[NSMALL + NGCLS - 1] = INT64_MAX;  // the single-panel big columns; bin NSMALL + NGCLS: thin ones
     static const char* el = getenv("CBG_GROUP_LOG_MAX");
     const int glmax = el ? std::max(0, std::min(GROUP_LOG_MAX, atoi(el))) : GROUP_LOG_MAX;
     for (int c = 0; c + 1 < NGCLS; ++c) {
@@ -2709,15 +2726,22 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       thr[NSMALL + c] = (groups && g <= bp.R && g <= (1LL << glmax)) ? gp * bp.R / g : -1;
     }
     BinPending sp;
-    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS - 1, big, sp, s, 0, B.cp, NSMALL);
+    const bool thin_on = !(getenv("CBG_THIN") && !strcmp(getenv("CBG_THIN"), "0"));  // read per call (tests)
+    thin_R = (fused && thin_on && bp.R >= 4) ? bp.R : 0;
+    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
+    if (thin_R && sp.hf[THIN_BIN] >= THIN_MAX_FLOPS) {
+      // too many thin products for the sort's temporaries: classify again without
+      thin_R = 0;
+      bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, 0, THIN_BIN);
+      CBG_HIP(hipStreamSynchronize(s));
+    }
     bin_scatter(nz, sp, sb, s, df);
-    big_entries = (int64_t)sp.big_entries;
+    big_entries = (int64_t)sp.big_entries[0];
+    thin_entries = (int64_t)sp.big_entries[1];
   }
   // small-column symbolic bins on the side stream, big columns on the main one
   // (bins 1-2 fused with their numeric unless CBG_FUSE_SMALL=0)
-  static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
-  const bool fused = fuse_small;
   DBuf<int32_t> fused_ir;
   DBuf<double> fused_val;
   DBuf<int64_t> fused_slot;  // temporary slot of each fused column (-1: none)
@@ -2748,8 +2772,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       // bins 1..8 (flops <= 256): symbolic and numeric in one pass into fused_ir/val
       for (int b = 1; b <= SYM_FUSED_LAST; ++b)
         fused_off[b + 1] = fused_off[b] + (size_t)sb.count[b] * (size_t)fmax_of(b);
-      fused_ir.reset(fused_off[SYM_FUSED_LAST + 1] + 1);
-      fused_val.reset(fused_off[SYM_FUSED_LAST + 1] + 1);
+      // the thin columns' unique entries follow the fused bins' slots
+      const size_t ftot = fused_off[SYM_FUSED_LAST + 1] + (thin_R ? (size_t)sb.flops[THIN_BIN] : 0);
+      fused_ir.reset(ftot + 1);
+      fused_val.reset(ftot + 1);
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) {
         if (semiring == CBG_MIN_PLUS)
           launch_esc<1>(at(b), sb.count[b], fmax_of(b), B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p,
@@ -2768,6 +2794,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, A, cnt.p, symst[11]);
     launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, A, cnt.p, symst[12]);
   }
+  if (thin_R && sb.count[THIN_BIN] > 0)
+    thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
+                 B, cmap.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
+                 (int64_t)fused_off[SYM_FUSED_LAST + 1], s, df);
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
   const int nbig = bp.nbig;
@@ -2875,7 +2905,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   BinPending npend;
-  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[SYM_FUSED_LAST] : 0);
+  bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[SYM_FUSED_LAST] : 0, B.cp,
+               MAXBINS, thin_R, 0);
   // compaction of C's columns (SpDCCols(SpTuples): nonempty columns only)
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
@@ -2972,9 +3003,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
-  if (fused && fused_off[SYM_FUSED_LAST + 1] > 0)
+  if (fused && (fused_off[SYM_FUSED_LAST + 1] > 0 || (thin_R && sb.count[THIN_BIN] > 0)))
+  {
     hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz * COPY_TPC, 256)), dim3(256), 0, snum, nz, fused_slot.p, cnt.p,
-                       colptr.p, fused_ir.p, fused_val.p, C.ir, C.val);
+                       colptr.p, fused_ir.p, fused_val.p, C.ir, C.val, (int64_t)fused_off[SYM_FUSED_LAST + 1]);
+    if (thin_R)
+      thin_copy(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], fused_slot.p, cnt.p, colptr.p, fused_ir.p,
+                fused_val.p, C.ir, C.val, s);
+  }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);

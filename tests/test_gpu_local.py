@@ -150,6 +150,41 @@ def test_small_column_esc(cbg, m):
     assert_tiles_equal(Cm, oracle_local(Ah, Bh, "minplus"))
 
 
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_thin_big_columns(cbg, sr):
+    # long B columns over A columns of ONE nonzero (GalerkinNew's S * (A*T)):
+    # flops per B entry 1 < R / 4, so they take the expand-sort-compress pass of
+    # cbg_thin.hip instead of R (column, panel) pairs; A's rows come from a small
+    # pool so that products collide; a few ordinary big and small columns too
+    rng = np.random.default_rng(21)
+    m, k = (1 << 20) + 37, 120000
+    pool = rng.choice(m, 30000, replace=False)
+    rowsA = rng.choice(pool, k)
+    Ah = dict(m=m, n=k, cp=np.arange(k + 1, dtype=np.int64), jc=np.arange(k, dtype=np.int32),
+              ir=rowsA.astype(np.int32), val=rng.uniform(0.5, 2.0, k))
+    hub = np.sort(rng.choice(m, 20000, replace=False))          # one long A column: a regular big column
+    Ah = dict(m=m, n=k + 1, cp=np.append(Ah["cp"], k + len(hub)).astype(np.int64),
+              jc=np.arange(k + 1, dtype=np.int32), ir=np.concatenate([Ah["ir"], hub]).astype(np.int32),
+              val=np.concatenate([Ah["val"], rng.uniform(0.5, 2.0, len(hub))]))
+    lens = list(rng.integers(4100, 30000, 24)) + list(rng.integers(1, 40, 200))
+    ir, cp = [], [0]
+    for L in lens:
+        ir.extend(np.sort(rng.choice(k, int(L), replace=False)))
+        cp.append(len(ir))
+    ir.extend([k])  # the hub column alone
+    cp.append(len(ir))
+    nB = len(cp) - 1
+    Bh = dict(m=k + 1, n=nB, cp=np.array(cp, np.int64), jc=np.arange(nB, dtype=np.int32),
+              ir=np.array(ir, np.int32), val=rng.uniform(-1.0, 1.0, len(ir)))
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr).to_host()
+    ref = oracle_local(Ah, Bh, sr)
+    if sr == "plus":
+        assert_tiles_equal(C, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+    else:
+        assert_tiles_equal(C, ref)
+    assert cbg.last_stats()["n_big"] == 1  # the thin columns left the (column, panel) path
+
+
 def test_big_columns_tall_matrix(cbg):
     # m > 2^20 rows exercises multi-pass bitmaps and hash-mode slabs
     rng = np.random.default_rng(7)
@@ -244,15 +279,19 @@ def test_panel_groups_tall_matrix(cbg, sr):
     assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh, sr))
 
 
-def test_panel_groups_65_panels(cbg):
+@pytest.mark.parametrize("thin", ["0", "1"])
+def test_panel_groups_65_panels(cbg, thin, monkeypatch):
     """m = 2^24 + 77 (65 row panels, the scale-24 case): columns of 4400-4800 products
     fall in the 32-panel group class (groups of up to 64 panels, GROUP_LOG_MAX = 6),
     one hash slab spanning 2^23 rows whose emit buckets need 17-bit row offsets;
-    bit-exact against the oracle, plus-times and min-plus."""
+    bit-exact against the oracle, plus-times and min-plus.  With the thin-column
+    pass on, the 20 columns of 600 B entries over 8-row A columns (flops x 4 <
+    entries x 65 panels) take it instead."""
+    monkeypatch.setenv("CBG_THIN", thin)
     Ah, Bh = _panel_group_operands((1 << 24) + 77)
     for sr in ("plus", "minplus"):
         C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr)
-        assert cbg.last_stats()["n_big"] > 300
+        assert cbg.last_stats()["n_big"] == (300 if thin == "1" else 320)
         assert_tiles_equal(C.to_host(), oracle_local(Ah, Bh, sr))
 
 
