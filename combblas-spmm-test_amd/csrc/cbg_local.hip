@@ -211,6 +211,13 @@ __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB
     part[blockIdx.x] = t;
   }
 }
+// flops when every A column has exactly one entry: the B column lengths, and
+// their total (nnz(B)) in flops[nz]
+__global__ void k_flops_unit(int64_t nz, const int64_t* __restrict__ cpB, int64_t* __restrict__ flops) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j < nz) flops[j] = cpB[j + 1] - cpB[j];
+  if (j == 0) flops[nz] = cpB[nz];
+}
 // total of part[0, n) into *out (one block)
 __global__ __launch_bounds__(1024) void k_sum_parts(const unsigned long long* __restrict__ part, int64_t n,
                                                     unsigned long long* __restrict__ out) {
@@ -1501,25 +1508,48 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
   }
 }
 
-// the fused columns' temporary slots -> C, in COLUMN order (tslot[col] >= 0:
-// the column's slot; -1: not fused): a wave's threads take consecutive
-// columns, so C's entries are written in order (a pass over the bins in their
-// perm order scattered its stores over C and gathered perm / cnt / colptr)
-constexpr int COPY_TPC = 4;  // threads per column
-__global__ void k_copy_fused(int64_t nz, const int64_t* __restrict__ tslot, const int32_t* __restrict__ cnt,
-                             const int64_t* __restrict__ colptr, const int32_t* __restrict__ tir,
-                             const double* __restrict__ tval, int32_t* __restrict__ out_ir,
-                             double* __restrict__ out_val, int64_t thin_base) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t col = t / COPY_TPC;
-  if (col >= nz) return;
-  const int64_t src = tslot[col];
-  if (src < 0 || src >= thin_base) return;  // not fused / a thin column (thin_copy)
-  const int c = cnt[col];
-  const int64_t o = colptr[col];
-  for (int e = (int)(t % COPY_TPC); e < c; e += COPY_TPC) {
-    out_ir[o + e] = tir[src + e];
-    out_val[o + e] = tval[src + e];
+// the fused columns' temporary slots -> C, in COLUMN order: a wave takes 64
+// consecutive columns, flattens the entries of its fused ones (tslot[col] in
+// [0, thin_base); -1: not fused, >= thin_base: a thin column, thin_copy) and
+// copies them one per lane, so the stores run along C (a few threads per
+// column, in bin order or column order, left C's lines written in pieces and
+// walked each column serially: 0.4 ms per GalerkinNew product)
+__global__ __launch_bounds__(256) void k_copy_fused(int64_t nz, const int64_t* __restrict__ tslot,
+                                                    const int32_t* __restrict__ cnt,
+                                                    const int64_t* __restrict__ colptr,
+                                                    const int32_t* __restrict__ tir, const double* __restrict__ tval,
+                                                    int32_t* __restrict__ out_ir, double* __restrict__ out_val,
+                                                    int64_t thin_base) {
+  const int64_t c0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE * WAVE;
+  if (c0 >= nz) return;
+  const int lane = lane_id();
+  const int64_t col = c0 + lane;
+  int64_t src = -1, dst = 0;
+  int c = 0;
+  if (col < nz) {
+    src = tslot[col];
+    if (src >= 0 && src < thin_base) {
+      c = cnt[col];
+      dst = colptr[col];
+    }
+  }
+  const int incl = wave_incl_scan(c);
+  const int total = wave_last(incl);
+  for (int q0 = 0; q0 < total; q0 += WAVE) {
+    const int q = q0 + lane;
+    int lo = 0, hi = WAVE - 1;  // the column of flattened entry q
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const int mid = (lo + hi) >> 1;
+      if (__shfl(incl, mid) > q) hi = mid; else lo = mid + 1;
+    }
+    const int64_t o_src = __shfl(src, lo), o_dst = __shfl(dst, lo);
+    const int o_ex = __shfl(incl - c, lo);
+    if (q < total) {
+      const int e = q - o_ex;
+      out_ir[o_dst + e] = tir[o_src + e];
+      out_val[o_dst + e] = tval[o_src + e];
+    }
   }
 }
 
@@ -2543,7 +2573,8 @@ __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __res
   }
 }
 // flops[0, nz) per B column and their total in flops[nz] (B.nnz > 0)
-static void launch_flops(const cbg_tile& B, const int2* cmap, int64_t* flops, hipStream_t s, DeferredFree& df) {
+static void launch_flops(const cbg_tile& B, const int2* cmap, bool A_one_per_col, int64_t* flops, hipStream_t s,
+                         DeferredFree& df) {
   const int64_t nz = B.nzc;
   static const bool classic = getenv("CBG_FLOPS_CLASSIC") && atoi(getenv("CBG_FLOPS_CLASSIC"));
   if (classic) {  // a lane group per column + hub tail (before round 3)
@@ -2554,6 +2585,12 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, int64_t* flops, hi
     hipLaunchKernelGGL(k_flops_tail, dim3((unsigned)std::min<int64_t>(nz, 1024)), dim3(256), 0, s, B.cp, B.ir, cmap,
                        nz, flops, longq.p);
     df.take(longq);
+    return;
+  }
+  if (A_one_per_col) {
+    // every A column holds exactly one entry (a restriction operator's
+    // transpose, GalerkinNew's S): flops(j) = nnz(B(:, j)), no gathers
+    hipLaunchKernelGGL(k_flops_unit, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, B.cp, flops);
     return;
   }
   const int64_t nb = (B.nnz + FSEG_E - 1) / FSEG_E;
@@ -2687,7 +2724,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
 
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
-  launch_flops(B, cmap.p, flops.p, s, df);
+  launch_flops(B, cmap.p, A.nnz == A.n && A.nzc == A.n, flops.p, s, df);
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
@@ -3005,7 +3042,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   if (fused && (fused_off[SYM_FUSED_LAST + 1] > 0 || (thin_R && sb.count[THIN_BIN] > 0)))
   {
-    hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz * COPY_TPC, 256)), dim3(256), 0, snum, nz, fused_slot.p, cnt.p,
+    hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, fused_slot.p, cnt.p,
                        colptr.p, fused_ir.p, fused_val.p, C.ir, C.val, (int64_t)fused_off[SYM_FUSED_LAST + 1]);
     if (thin_R)
       thin_copy(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], fused_slot.p, cnt.p, colptr.p, fused_ir.p,
