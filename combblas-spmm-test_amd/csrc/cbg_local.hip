@@ -3037,6 +3037,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) fused_w += 0.25 * (double)sb.flops[b];
     numst[0] = numst[9] = snum;
     balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst);
+    // CBG_NUM_MAIN: bit b puts numeric bin b on the main stream, ahead of the
+    // slabs (a bin whose LDS table cannot sit beside the persistent bitmap
+    // slabs otherwise waits for them on the side stream and runs after them)
+    static const int num_main = getenv("CBG_NUM_MAIN") ? (int)strtol(getenv("CBG_NUM_MAIN"), nullptr, 0) : 0;
+    for (int b = 1; b <= 8; ++b)
+      if ((num_main >> b) & 1) numst[b] = s;
   }
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
