@@ -1379,7 +1379,7 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
                                                   int64_t* __restrict__ tslot) {
   constexpr int LOGC = CPW <= 1 ? 0 : CPW <= 2 ? 1 : CPW <= 4 ? 2 : CPW <= 8 ? 3 : CPW <= 16 ? 4 : 5;
   static_assert((1 << LOGC) == CPW && CPW <= 32, "columns per wave");
-  static_assert(NPL == 1 || NPL == 2 || NPL == 4, "products per lane");
+  static_assert(NPL == 1 || NPL == 2 || NPL == 4 || NPL == 8, "products per lane");
   constexpr int SH = 31 - LOGC;
   const int lane = lane_id();
   const int64_t idx0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE * CPW;
@@ -2143,10 +2143,14 @@ static void set_lds(K kernel, size_t bytes) {
 // bins of the symbolic phase (key = flops)
 //  0: F == 0 | 1: <=32 wave T64 | 2: <=128 wave T256 | 3: <=512 wave T1024 |
 //  4: <=1024 block T2048 | 5: <=2048 block T4096 | 6: <=4096 block T8192 | 7: big
-// symbolic bins: 1-8 (flops <= 2 ... 256) expand-sort-compress waves of 32 ... 1
-// columns (symbolic and numeric in one pass), 9 (<= 512) wave hash, 10-12 block hash
+// symbolic bins: 1-9 (flops <= 2 ... 512) expand-sort-compress waves of 32 ... 1
+// columns (symbolic and numeric in one pass; CBG_SYM_FUSED_LAST = 8 leaves bin 9
+// to the wave hash), 10-12 block hash
+#ifndef CBG_SYM_FUSED_LAST
+#define CBG_SYM_FUSED_LAST 9
+#endif
 static const int64_t kSymThr[] = {0, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 2048, 4096};
-constexpr int SYM_FUSED_LAST = 8;
+constexpr int SYM_FUSED_LAST = CBG_SYM_FUSED_LAST;
 // columns with more flops than this take the bitmap+rank slab path (runtime
 // override: CBG_BIG_FLOPS); it must stay <= 4096 so that every other column's
 // nnz fits the largest numeric hash bin
@@ -2193,12 +2197,13 @@ static void launch_esc1(const int32_t* perm, int n, int fmax, const cbg_tile& B,
 }
 // expand-sort-compress bin of flops <= fmax: CPW = 64 * NPL / fmax columns per
 // wave (one column per wave when A's rows leave no room for the column bits of
-// the sort key); fmax 128 / 256 sort 2 / 4 products per lane
+// the sort key); fmax 128 / 256 / 512 sort 2 / 4 / 8 products per lane
 template <int SR>
 static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
                        const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
                        hipStream_t s) {
   if (n <= 0) return;
+  if (fmax > 4 * WAVE) return launch_esc1<1, 8, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
   if (fmax > 2 * WAVE) return launch_esc1<1, 4, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
   if (fmax > WAVE) return launch_esc1<1, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
   int cpw = 1;
@@ -2784,7 +2789,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<int64_t> fused_slot;  // temporary slot of each fused column (-1: none)
   size_t fused_off[SYM_FUSED_LAST + 2] = {};  // temporary slots of the fused bins 1..SYM_FUSED_LAST
   // slot width of fused bin b: its flops bound (big >= 64 never clips bins 1..6,
-  // and a clipped bin 7 / 8 holds columns of <= big flops)
+  // and a clipped bin 7 .. 9 holds columns of <= big flops)
   auto fmax_of = [&](int b) { return (int)kSymThr[b]; };
   if (fused) {
     fused_slot.reset(nz);
@@ -2806,7 +2811,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const int32_t* P = sb.perm.p;
     auto at = [&](int b) { return P + sb.offset[b]; };
     if (fused) {
-      // bins 1..8 (flops <= 256): symbolic and numeric in one pass into fused_ir/val
+      // bins 1..SYM_FUSED_LAST (flops <= 512): symbolic and numeric in one pass into fused_ir/val
       for (int b = 1; b <= SYM_FUSED_LAST; ++b)
         fused_off[b + 1] = fused_off[b] + (size_t)sb.count[b] * (size_t)fmax_of(b);
       // the thin columns' unique entries follow the fused bins' slots
@@ -2826,7 +2831,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       for (int b = 6; b <= 7; ++b) launch_sym_wave<8>(at(b), sb.count[b], B, cmap.p, A, cnt.p, symst[b]);
       launch_sym_wave<10>(at(8), sb.count[8], B, cmap.p, A, cnt.p, symst[8]);
     }
-    launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
+    static_assert(SYM_FUSED_LAST == 8 || SYM_FUSED_LAST == 9, "fused bins");
+    if (!fused || SYM_FUSED_LAST < 9) launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
     launch_sym_block<11, 256>(at(10), sb.count[10], B, cmap.p, A, cnt.p, symst[10]);
     launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, A, cnt.p, symst[11]);
     launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, A, cnt.p, symst[12]);

@@ -113,8 +113,8 @@ def _sparse_cols(rng, m, lens, dup_rows=None):
 
 @pytest.mark.parametrize("m", [5000, (1 << 27) + 5])
 def test_small_column_esc(cbg, m):
-    # columns of <= 256 products run through the expand-sort-compress waves
-    # (k_esc_wave: 32 ... 1 columns per wave, 1, 2 or 4 products per lane); rows
+    # columns of <= 512 products run through the expand-sort-compress waves
+    # (k_esc_wave: 32 ... 1 columns per wave, 1, 2, 4 or 8 products per lane); rows
     # concentrated on few values force duplicate keys inside a wave, B columns
     # of many entries on empty A columns force several staging rounds, and
     # m >= 2^27 leaves no room for column bits in the sort key (CPW = 1)
@@ -128,7 +128,7 @@ def test_small_column_esc(cbg, m):
     nB = 3000
     ir, cp = [], [0]
     for j in range(nB):
-        target = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 100, 128, 160, 200, 256]))
+        target = int(rng.choice([1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64, 100, 128, 160, 200, 256, 300, 400, 512]))
         ks, f = [], 0
         for kk in rng.permutation(k):
             L = int(lensA[kk])
@@ -136,7 +136,7 @@ def test_small_column_esc(cbg, m):
                 continue
             ks.append(kk)
             f += L
-            if f == target or len(ks) > 90:
+            if f == target or len(ks) > 200:
                 break
         ks = sorted(ks) if ks else [int(np.argmax(lensA == 0))]
         ir.extend(ks)
