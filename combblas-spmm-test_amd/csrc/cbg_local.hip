@@ -2769,7 +2769,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     }
     BinPending sp;
     const bool thin_on = !(getenv("CBG_THIN") && !strcmp(getenv("CBG_THIN"), "0"));  // read per call (tests)
-    thin_R = (fused && thin_on && bp.R >= 4) ? bp.R : 0;
+    // CBG_THIN_RATIO (default 4): thin when flops * ratio < B entries * R
+    const char* tr = getenv("CBG_THIN_RATIO");
+    const int ratio = tr ? std::max(1, atoi(tr)) : (int)THIN_RATIO;
+    thin_R = (fused && thin_on && bp.R >= 4) ? (int)(bp.R * THIN_RATIO / ratio) : 0;
     bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
     if (thin_R && sp.hf[THIN_BIN] >= THIN_MAX_FLOPS) {
