@@ -519,6 +519,10 @@ constexpr int NFINE_MAX = 1 << (PANEL_LOG_MAX - FINE_LOG);  // fine ranges (= ma
 #define CBG_BIG_BS 512
 #endif
 constexpr int BIG_BS = CBG_BIG_BS;
+#ifndef CBG_PAIR_LOAD_NUM  // symbolic hash of a (column, panel) pair: T >= (NUM/DEN) * products
+#define CBG_PAIR_LOAD_NUM 2
+#define CBG_PAIR_LOAD_DEN 1
+#endif
 #ifndef CBG_SPARSE_SLAB_MAX
 #define CBG_SPARSE_SLAB_MAX 4096
 #endif
@@ -698,7 +702,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     hook(1);
     phase_mark(tmark, 8);
     int T = 512;
-    while (T < 2 * total) T <<= 1;
+    while (T * CBG_PAIR_LOAD_DEN < CBG_PAIR_LOAD_NUM * total) T <<= 1;
     if (total <= SPARSE_SLAB_MAX && T <= pwords) {
       if (c_dbg & 256) {
         __syncthreads();
