@@ -1243,84 +1243,6 @@ __global__ __launch_bounds__(256) void k_num_wave(const int32_t* __restrict__ pe
   }
 }
 
-// Small columns in ONE pass (flops <= 32 or <= 128: the first two symbolic
-// bins): a column with F products has at most F nonzeros, so its whole product
-// -- hash accumulate, sort -- runs in the symbolic phase into a temporary slot
-// of FMAX = the bin's flops bound entries (idx * FMAX: no scan needed), and the
-// count goes to cnt[col].  After the column pointers are known, k_copy_fused
-// moves each slot's entries to C.  The symbolic hash pass of these columns
-// (estimateNNZ_Hash for them) disappears; the temporary costs 24 B per entry.
-// GalerkinNew's products (mostly columns of <= 32 products) are dominated by it.
-template <int LOGT, int SR, int FMAX>
-__global__ __launch_bounds__(256) void k_fused_wave(const int32_t* __restrict__ perm, int n,
-                                                    const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                    const double* __restrict__ valB, const int2* __restrict__ cmap,
-                                                    const int32_t* __restrict__ irA, const double* __restrict__ valA,
-                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ tir,
-                                                    double* __restrict__ tval) {
-  constexpr int T = 1 << LOGT;
-  static_assert(T >= 2 * FMAX || T == WAVE, "table sizes of the symbolic bins");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int w = threadIdx.x / WAVE, lane = lane_id();
-  char* base = smem + w * NumWaveLds<LOGT>::BYTES;
-  double* vals = reinterpret_cast<double*>(base);
-  double* bv = vals + T;
-  int* keys = reinterpret_cast<int*>(bv + WAVE);
-  int* pref = keys + T;
-  int* st = pref + WAVE + 4;
-  const int idx = blockIdx.x * (blockDim.x / WAVE) + w;
-  if (idx >= n) return;
-  const int col = perm[idx];
-  for (int j = lane; j < T; j += WAVE) {
-    keys[j] = EMPTY_KEY;
-    vals[j] = Sem<SR>::identity();
-  }
-  const int64_t p1 = cpB[col + 1];
-  for (int64_t c0 = cpB[col]; c0 < p1; c0 += WAVE) {
-    const int64_t p = c0 + lane;
-    int s = 0, len = 0;
-    double bval = 0.0;
-    if (p < p1) {
-      int2 e = cmap[irB[p]];
-      s = e.x;
-      len = e.y;
-      bval = valB[p];
-    }
-    const int incl = wave_incl_scan(len);
-    const int total = wave_last(incl);
-    pref[lane + 1] = incl;
-    if (lane == 0) pref[0] = 0;
-    st[lane] = seg_stage(s, incl - len);
-    bv[lane] = bval;
-    wave_sync();
-    wave_products(
-        pref, WAVE, 0, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
-        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
-        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
-    wave_sync();
-  }
-  const int64_t o = (int64_t)idx * FMAX;
-  if constexpr (T == WAVE) {  // one slot per lane: sort in registers
-    int key = keys[lane];
-    double val = vals[lane];
-    const int nout = __popcll(__ballot(key != EMPTY_KEY));
-    wave_bitonic_sort_kv(key, val, lane);
-    if (lane < nout) {
-      tir[o + lane] = key;
-      tval[o + lane] = val;
-    }
-    if (lane == 0) cnt[col] = nout;
-    return;
-  }
-  int nout = 0;
-  for (int j = lane; j < T; j += WAVE) nout += __popcll(__ballot(keys[j] != EMPTY_KEY));
-  bitonic_sort_kv<T, WAVE>(keys, vals, lane, WaveSync());
-  for (int e = lane; e < nout; e += WAVE) {
-    tir[o + e] = keys[e];
-    tval[o + e] = vals[e];
-  }
-  if (lane == 0) cnt[col] = nout;
-}
 // Small columns by expand-sort-compress in registers (flops <= fmax = 64 *
 // NPL / CPW per column): a wave takes CPW consecutive columns of its bin,
 // expands their <= 64 * NPL products (NPL per lane, product q in register q /
@@ -2179,15 +2101,6 @@ static void launch_sym_wave(const int32_t* perm, int n, const cbg_tile& B, const
   const size_t lds = 4 * SymWaveLds<LOGT>::INTS * sizeof(int);
   set_lds(k_sym_wave<LOGT>, lds);
   hipLaunchKernelGGL(k_sym_wave<LOGT>, dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, cmap, A.ir, cnt);
-}
-template <int LOGT, int SR, int FMAX>
-static void launch_fused(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
-                         int32_t* cnt, int32_t* tir, double* tval, hipStream_t s) {
-  if (n <= 0) return;
-  const size_t lds = 4 * NumWaveLds<LOGT>::BYTES;
-  set_lds(k_fused_wave<LOGT, SR, FMAX>, lds);
-  hipLaunchKernelGGL((k_fused_wave<LOGT, SR, FMAX>), dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, B.val,
-                     cmap, A.ir, A.val, cnt, tir, tval);
 }
 // expand-sort-compress bin b (flops <= fmax = 64 >> (b - 1)... as CPW = 64 / fmax
 // columns per wave; one column per wave when A's rows leave no room for the
