@@ -1003,6 +1003,33 @@ def test_local_digest_large_vs_oracle(cbg, scale, sr):
         assert d["nnz"] == sym["nnzC"]
 
 
+def test_local_scale24_column_pieces_vs_oracle(cbg):
+    """Scale 24 (2^24 rows: R = 64 row panels, groups of up to 64 panels) pinned
+    against the CPU oracle on a sample of C: column pieces p of 512 (B = A's
+    columns [p n/512, (p+1) n/512), the slicing of tools/oracle_digest_pieces.py),
+    each one local multiply on the GPU digested at its column offset, equal to the
+    oracle's piece digest (tests/golden/oracle_large.json s24_ef16_pieces: the
+    first pieces; the whole C, 183 G nonzeros, takes the oracle ~7 h on 6 cores)."""
+    g = _oracle_large("s24_ef16_pieces")
+    n = 1 << 24
+    A = cbg.rmat_tile(24, 16)
+    for key, ref in sorted(g["digests"].items(), key=lambda kv: int(kv[0])):
+        ph = int(key)
+        c0, c1 = ph * (n // g["pieces"]), (ph + 1) * (n // g["pieces"])
+        left, right = A.split_cols(c1)
+        right.free()
+        low, B = left.split_cols(c0)
+        low.free()
+        left.free()
+        C = cbg.LocalHybridSpGEMM(A, B)
+        d = C.digest(0, c0)
+        C.free()
+        B.free()
+        assert (d["nnz"], d["nzc"], d["hs"], d["hv"]) == (ref["nnz"], ref["nzc"], ref["hs"], ref["hv"]), (ph, d, ref)
+        assert d["unsorted"] == 0
+    A.free()
+
+
 def test_local_scale22_ef8_resident(cbg):
     """SURVEY 8(d)'s scale-22 ef8 case: one local multiply whose C (9.08 G nonzeros,
     109 GB) stays resident on the GPU; its digest equals the oracle's
