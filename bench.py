@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--phase-consumer", choices=["none", "digest"], default="none",
                    help="what the phase callback does with each phase's device C tile")
     p.add_argument("--grid", default=None, help="RxC process grid (default: GRIDS[N])")
+    p.add_argument("--values", choices=["rmat", "random"], default="rmat",
+                   help="rmat: the generator's duplicate counts (small integers); random: U[-1,1) from a hash of "
+                        "(row, col) on the same structure (SURVEY 8(d)'s fp variant; A's values are then f64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0, help="default: the CPUs this job may use")
     p.add_argument("--cpu-scale", type=int, default=20, help="scale of the CPU-baseline sample (reference Synch)")
@@ -202,14 +205,14 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     N = max(world, 1)
     scale = a.scale if a.scale is not None else 22
-    # phases: 0 (default) = MemEfficientSpGEMM picks them from device memory on
+    # phases: PHASES_AUTO (default) = MemEfficientSpGEMM picks them from device memory on
     # every call, inside the timed step (ParFriends.h:482-535; see
     # cbg_summa_spgemm_memeff): scale 22 on one GPU (C = 297 GB) streams C per
     # B-column phase, a C tile that fits runs as one phase (the adaptive
     # double-buffered DoubleBuff).  --phases 1 keeps C resident (Mult_AnXBn_*),
     # --phases P > 1 forces P phases.
     if a.phases is None:
-        a.phases = 0
+        a.phases = -1  # PHASES_AUTO
     stream_c = a.phases != 1
     rehearsal = N > 1 and os.environ.get("CBG_RANK_HOSTIDS") == "1"
     if rehearsal:
@@ -261,6 +264,11 @@ def main():
     t_gen = time.perf_counter()
     A = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)
     B = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)  # deep copy (aliasing is forbidden)
+    if a.values == "random":
+        r0_ = cbg.block_range(1 << scale, grid.grid_rows, grid.prow)[0]
+        c0_ = cbg.block_range(1 << scale, grid.grid_cols, grid.pcol)[0]
+        A.tile.set_random_values(row_off=r0_, col_off=c0_)
+        B.tile.set_random_values(row_off=r0_, col_off=c0_)
     cbg.synchronize()
     t_gen = time.perf_counter() - t_gen
     mult = cbg.Mult_AnXBn_DoubleBuff if a.algo == "doublebuff" else cbg.Mult_AnXBn_Synch
@@ -331,7 +339,7 @@ def main():
 
     phases_run = plans[-1]["phases"] if plans else 1
     if rank == 0:
-        traffic, traffic_src = pmc_traffic(scale, a.ef, phases_run) if N == 1 else (None, None)
+        traffic, traffic_src = pmc_traffic(scale, a.ef, phases_run) if N == 1 and a.values == "rmat" else (None, None)
         peaks += [cbg.hbm_copy_bandwidth(4 << 30, 10) for _ in range(2)]
         peak_measured = max(peaks)
         out = {
@@ -347,7 +355,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic Graph500 R-MAT (SEED 0xDECAFBAD), generated on device",
+            "data": "synthetic Graph500 R-MAT (SEED 0xDECAFBAD), generated on device" + (
+                "; values U[-1,1) from a hash of (row, col)" if a.values == "random" else ""),
             "timing": {"value_from": "median over the steps of (barrier; step; synchronize) max over ranks "
                                      "(BASELINE.md: median of >= 5)",
                        "step_ms": [round(x * 1e3, 3) for x in step_s],
@@ -355,6 +364,7 @@ def main():
             "config": {"workload": "R-MAT scale-%d ef%d A·A, Mult_AnXBn_%s, %s" % (
                 scale, a.ef, "DoubleBuff" if a.algo == "doublebuff" else "Synch", a.exec_mode),
                 "scale": scale, "edgefactor": a.ef, "grid": "%dx%d" % (grid.grid_rows, grid.grid_cols),
+                "values": a.values,
                 "nnz_C": nnz_c, "flops": flops, "gen_s": round(t_gen, 3),
                 "big_columns": st["n_big"], "slabs": st["n_slabs"], "transport": transport,
                 "phases": phases_run,
@@ -363,18 +373,26 @@ def main():
                                 "c_budget_gb_rank0": round(plans[-1]["c_budget_bytes"] / 1e9, 1),
                                 "oom_splits": plans[-1]["oom_splits"],
                                 "plan_ms_per_step": [round(p_["plan_ms"], 2) for p_ in plans[-a.steps:]],
-                                "rule": "MemEfficientSpGEMM(phases=0): flops of the rank's product from tile count "
+                                "rule": "MemEfficientSpGEMM(phases=PHASES_AUTO): flops of the rank's product from tile count "
                                         "vectors (x the compression of an exact symbolic of a sample when the flops "
                                         "bound asks for > 1 phase), 12 B per entry against 60 % of the free HBM, "
                                         "inside each timed step"}
                                if plans else None),
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
+                                     "decision": [["one piece", "pipelined", "adaptive: pipelined",
+                                                   "adaptive: rejoined"][p_["rule"]] for p_ in pipe],
+                                     "bytes_bcast_rank0": [p_["bytes_recv"] for p_ in pipe],
+                                     "exposed_comm_ms": [round(p_["exposed_comm_ms"], 3) for p_ in pipe],
                                      "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],
                                      "est_hidden_ms": [round(p_["est_hidden_ms"], 3) for p_ in pipe],
                                      "piece_cost_ms": [round(p_["piece_cost_ms"], 3) for p_ in pipe],
-                                     "rule": "B-column pieces broadcast one ahead when the measured first-piece "
-                                             "broadcast, scaled to the rest, exceeds what an extra piece costs: "
-                                             "max(3 ms, 4 % of the previous step's local multiply)"}
+                                     "rule": "the A block row's gather and B piece 0 (1/8 of the columns) in one "
+                                             "broadcast group; on RCCL grids with > 1 remote B tile per grid column "
+                                             "piece 1 is broadcast while piece 0 multiplies; with one remote B tile "
+                                             "(or the host transport) only when the first group's measured time, "
+                                             "scaled to the rest, exceeds what an extra piece costs: max(3 ms, 4 % of "
+                                             "the previous step's local multiply).  exposed_comm_ms = rank 0's "
+                                             "compute-stream waits for the broadcasts (HIP events)"}
                 if N > 1 else None,
                 "C": "materialized per phase in HBM, handed to a %s consumer" % a.phase_consumer if stream_c
                      else "resident in HBM"},

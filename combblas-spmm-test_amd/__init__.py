@@ -36,6 +36,8 @@ LIB_PATH = os.environ.get("CBG_LIB") or os.path.join(_HERE, "libcbg.so")
 PLUS_TIMES, MIN_PLUS = 0, 1
 DOUBLEBUFF, SYNCH = 0, 1
 EXEC_PANEL, EXEC_STAGED = 0, 1
+RANDOM_VALUES_SEED = 0x5EEDF00D  # Tile.set_random_values default
+PHASES_AUTO = -1  # MemEfficientSpGEMM: phase count from the device's free memory (include/cbg.h CBG_PHASES_AUTO)
 
 GRIDMISMATCH, DIMMISMATCH, NOTSQUARE, MATRIXALIAS, INVALIDPARAMS = 3001, 3002, 3003, 3005, 3007
 HIPERROR, RCCLERROR, OOM, NOTSUPPORTED = 3100, 3101, 3102, 3103
@@ -70,8 +72,10 @@ EXPORTS = [
     "cbg_last_stats", "cbg_get_unique_id", "cbg_grid_create", "cbg_grid_create_host", "cbg_grid_destroy",
     "cbg_grid_info", "cbg_grid_barrier", "cbg_grid_allreduce_max", "cbg_grid_allreduce_sum_i64", "cbg_summa_spgemm",
     "cbg_tile_equal", "cbg_summa_spgemm_phased", "cbg_tile_transpose", "cbg_tile_dim_apply", "cbg_restriction_tile",
+    "cbg_tile_random_values",
     "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
     "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info", "cbg_summa_spgemm_memeff",
+    "cbg_last_summa_comm",
     "cbg_last_phase_plan",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
@@ -135,6 +139,7 @@ def lib():
         "cbg_tile_transpose": ([T, T], i32),
         "cbg_tile_dim_apply": ([T, i32, ctypes.POINTER(ctypes.c_double), i32], i32),
         "cbg_restriction_tile": ([i32, i32, ctypes.c_uint64, i32, i32, i32, i32, T], i32),
+        "cbg_tile_random_values": ([T, ctypes.c_uint64, i64, i64], i32),
         "cbg_grid_transpose": ([vp, T, T], i32),
         "cbg_grid_block_extract": ([vp, T, i64, i64, i32, i64, i64, T], i32),
         "cbg_grid_agree": ([vp, i32, ctypes.POINTER(i32)], i32),
@@ -144,8 +149,12 @@ def lib():
         "cbg_device_memory": ([ctypes.POINTER(ctypes.c_size_t)] * 2, i32),
         "cbg_last_summa_info": ([ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], i32),
+        "cbg_last_summa_comm": ([ctypes.POINTER(i32), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double)], i32),
     }
+    experiment = "CBG_LIB" in os.environ  # an older build under A/B may lack the newest entry points
     for name, (args, res) in sig.items():
+        if experiment and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -236,6 +245,12 @@ class Tile:
             raise CbgError(INVALIDPARAMS, "DimApply vector length does not match the tile")
         _check(lib().cbg_tile_dim_apply(ctypes.byref(self.c), dim, v.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                         _OPS.get(op, op)))
+
+    def set_random_values(self, seed=RANDOM_VALUES_SEED, row_off=0, col_off=0):
+        """Values U[-1, 1) from a hash of (seed, global column, global row) (SURVEY 8(d)'s
+        random-valued inputs; the tile's global offsets make it grid-independent); in place."""
+        _check(lib().cbg_tile_random_values(ctypes.byref(self.c), seed, int(row_off), int(col_off)))
+        return self
 
     def split_cols(self, cut):
         """SpDCCols::Split (SpDCCols.cpp:905-930)"""
@@ -387,7 +402,11 @@ def summa_info():
     to cost (pipelined when the hidden broadcast is worth it)."""
     a, b, c, d = ctypes.c_int(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
     lib().cbg_last_summa_info(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d))
-    return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value, piece_cost_ms=d.value)
+    r, nb, ex = ctypes.c_int(), ctypes.c_int64(), ctypes.c_double()
+    if hasattr(lib(), "cbg_last_summa_comm"):  # (absent only from older builds under A/B)
+        lib().cbg_last_summa_comm(ctypes.byref(r), ctypes.byref(nb), ctypes.byref(ex))
+    return dict(pieces=a.value, bcast_ms_piece0=b.value, est_hidden_ms=c.value, piece_cost_ms=d.value,
+                rule=r.value, bytes_recv=nb.value, exposed_comm_ms=ex.value)
 
 
 def phase_plan():
@@ -985,9 +1004,10 @@ def MemEfficientSpGEMM(A, B, phases, sr=PlusTimesSRing, algo=DOUBLEBUFF, exec_mo
     """ParFriends.h:449-730 with `phases` column pieces of B; the MCL pruning
     arguments must stay at their no-pruning values (pruning is not on this path).
 
-    perProcessMemory > 0 (GB, ParFriends.h:482-535) or phases <= 0 (this
+    perProcessMemory > 0 (GB, ParFriends.h:482-535) or phases == PHASES_AUTO (this
     library's extension: the device's free memory) picks the phase count from
-    memory (see cbg_summa_spgemm_memeff; phase_plan() reports it).
+    memory (see cbg_summa_spgemm_memeff; phase_plan() reports it); otherwise
+    phases < 1 or >= the inner dimension is reset to 1 (ParFriends.h:468-473).
 
     on_phase=None: C is the column concatenation of the phase products
     (ColConcatenate).  on_phase=fn: fn(phase, col_offset, Tile) is called with

@@ -269,6 +269,15 @@ int cbg_restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, in
   });
 }
 
+int cbg_tile_random_values(cbg_tile* t, uint64_t seed, int64_t row_off, int64_t col_off) {
+  if (int rc = check_tile(t, true, "tile")) return rc;
+  if (row_off < 0 || col_off < 0) return fail(CBG_ERR_INVALIDPARAMS, "negative offsets");
+  return guard([&] {
+    cbg::tile_random_values(*t, seed, row_off, col_off, default_stream());
+    return CBG_OK;
+  });
+}
+
 static const char* summa_msg(int rc);
 
 int cbg_grid_transpose(cbg_grid* g, const cbg_tile* local, cbg_tile* out) {
@@ -514,6 +523,14 @@ int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden
   if (bcast_ms_piece0) *bcast_ms_piece0 = i.bcast_ms_piece0;
   if (est_hidden_ms) *est_hidden_ms = i.est_hidden_ms;
   if (piece_cost_ms) *piece_cost_ms = i.piece_cost_ms;
+  return CBG_OK;
+}
+
+int cbg_last_summa_comm(int* rule, int64_t* bytes_recv, double* exposed_comm_ms) {
+  const cbg::SummaInfo& i = cbg::summa_info();
+  if (rule) *rule = i.rule;
+  if (bytes_recv) *bytes_recv = i.bytes_recv;
+  if (exposed_comm_ms) *exposed_comm_ms = i.exposed_comm_ms;
   return CBG_OK;
 }
 

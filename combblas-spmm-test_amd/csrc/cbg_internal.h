@@ -50,6 +50,9 @@ class DevicePool {
   void* reserve_growable(size_t max_bytes);
   void grow(void* base, size_t bytes);  // map [base, base + bytes)
   size_t bytes_in_use() const { return in_use_; }
+  // allocation serial of the live block that contains p (a block handed out
+  // again gets a new one); 0 if p is not in a live pool block
+  uint64_t serial_of(const void* p);
   size_t bytes_cached() const { return cached_; }
   ~DevicePool() { trim(); }
 
@@ -64,6 +67,8 @@ class DevicePool {
   std::map<void*, size_t> live_;
   std::map<void*, Growable> grow_;        // growable blocks in use
   std::map<void*, Growable> grow_cache_;  // freed growable blocks, still mapped, reused first
+  std::map<void*, uint64_t> serial_;      // live blocks (regular and growable) -> allocation serial
+  uint64_t next_serial_ = 0;
   size_t in_use_ = 0, cached_ = 0;
 };
 DevicePool& pool();
@@ -168,6 +173,11 @@ struct SummaInfo {
   int pieces = 0;
   double bcast_ms_piece0 = 0, est_hidden_ms = 0, piece_cost_ms = 0;
   int oom_splits = 0;  // phases computed as column halves after an out-of-memory
+  // 0: one piece, no decision; 1: pipelined (RCCL, > 1 remote B tile);
+  // 2: adaptive, kept two pieces; 3: adaptive, rejoined into one
+  int rule = 0;
+  int64_t bytes_recv = 0;      // A and B tile bytes this rank received
+  double exposed_comm_ms = 0;  // compute-stream waits for the broadcasts (events)
 };
 // the last MemEfficientSpGEMM call's phase plan: phases run, and when they
 // were chosen from memory, this rank's product flops, estimated nnz(C) and
@@ -183,7 +193,9 @@ SummaInfo& summa_info();
 // A-side preparation (column maps of A) kept across the local multiplies of
 // one MemEfficientSpGEMM call, whose phases all multiply the same A: between
 // aprep_begin() and aprep_end() on a thread, a local multiply whose A has the
-// same arrays and sizes as the previous one reuses its maps.
+// same arrays, the same pool allocations of them (DevicePool::serial_of: a
+// freed and re-allocated block at the same address is a different A) and the
+// same sizes as the previous one reuses its maps.
 void aprep_begin();
 void aprep_end();
 struct APrepScope {
@@ -207,6 +219,16 @@ void thin_columns(const int32_t* perm, int n, int64_t E, int64_t fthin, const cb
                   int64_t base, hipStream_t s, DeferredFree& df);
 void thin_copy(const int32_t* perm, int n, const int64_t* tslot, const int32_t* cnt, const int64_t* colptr,
                const int32_t* tir, const double* tval, int32_t* out_ir, double* out_val, hipStream_t s);
+
+// radix sort of (key, value) pairs (cbg_sort.hip): LSD over the 8-bit digits
+// that `varying` marks as possibly nonzero, stable, 64-bit counts; the sorted
+// pairs end in `keys` / `vals` (the DBufs may be swapped with temporaries)
+template <typename K>
+void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned long long varying, hipStream_t s);
+// equal consecutive keys combined with the semiring's add (in order); returns the runs
+template <typename K>
+int64_t reduce_by_key(const K* keys, const double* vals, int64_t n, int semiring, K* ukeys, double* uvals,
+                      hipStream_t s);
 
 // multiway merge of column-sorted partial tiles (cbg_merge.hip)
 // int64 entry counts: column chunks of < 2^30 stacked entries (CBG_MERGE_CHUNK
@@ -268,6 +290,8 @@ void tile_transpose(const cbg_tile& T, cbg_tile& out, hipStream_t s);
 void tile_dim_apply(cbg_tile& t, int dim, const double* vec_host, int op, hipStream_t s);
 void restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile& out,
                       hipStream_t s);
+// values U[-1, 1) from a hash of (seed, global column, global row) (test inputs)
+void tile_random_values(cbg_tile& t, uint64_t seed, int64_t roff, int64_t coff, hipStream_t s);
 
 // measured HBM bandwidth: 16-B-per-lane device copy (cbg_ops.hip)
 double hbm_copy_gbps(int64_t bytes, int reps);

@@ -378,6 +378,79 @@ __device__ __forceinline__ void hash_acc_t(int* keys, double* vals, int row, dou
     h = h + 1 == T ? 0u : h + 1;
   }
 }
+// the same from probe position h on (an overflow item resumes where it stopped)
+template <int SR, int T>
+__device__ __forceinline__ void hash_acc_from(int* keys, double* vals, int row, double v, unsigned h) {
+  while (true) {
+    const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+    if (old == EMPTY_KEY || old == row) {
+      Sem<SR>::lds_acc(&vals[h], v);
+      return;
+    }
+    h = h + 1 == T ? 0u : h + 1;
+  }
+}
+
+// Bounded probing with a block overflow list.  A wave's linear-probe loop
+// runs until its slowest lane has found a slot: at load 2/3 that is ~10 CAS
+// wave-instructions per 64 products (rocprofv3, scale 22: the LDS array 70 %
+// busy in the hash slabs), although a single lane needs ~2.  Here every lane
+// makes at most NPROBE probes; a product still without a slot is appended to
+// an LDS list (one atomic per wave) and inserted after the product loop by
+// dense waves, resuming at probe NPROBE.  A full list falls back to inline
+// probing (correct, slower).
+struct HashOvf {
+  int* count;    // LDS counter (reset by the caller before the product loop)
+  int* row;      // [cap]
+  double* val;   // [cap]
+  int cap;
+};
+__device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+template <int SR, int T, int NPROBE>
+__device__ __forceinline__ void hash_acc_bounded(int* keys, double* vals, int row, double v, const HashOvf& o) {
+  unsigned h = hash_slot_t<T>(row);
+  bool done = false;
+#pragma unroll
+  for (int k = 0; k < NPROBE; ++k) {
+    if (!done) {
+      const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+      if (old == EMPTY_KEY || old == row) {
+        Sem<SR>::lds_acc(&vals[h], v);
+        done = true;
+      } else {
+        h = h + 1 == T ? 0u : h + 1;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(!done);
+  if (m) {  // uniform over the wave's active lanes
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane_id() == leader) base = atomicAdd(o.count, __popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (!done) {
+      const int idx = base + lane_rank(m);
+      if (idx < o.cap) {
+        o.row[idx] = row;
+        o.val[idx] = v;
+      } else {
+        hash_acc_from<SR, T>(keys, vals, row, v, h);
+      }
+    }
+  }
+}
+// the overflow list's items, inserted by the whole block (call after a barrier)
+template <int SR, int T, int NPROBE, int BS>
+__device__ __forceinline__ void hash_ovf_drain(int* keys, double* vals, const HashOvf& o, int n) {
+  for (int i = threadIdx.x; i < n; i += BS) {
+    const int row = o.row[i];
+    unsigned h = hash_slot_t<T>(row) + NPROBE;
+    while (h >= (unsigned)T) h -= T;
+    hash_acc_from<SR, T>(keys, vals, row, o.val[i], h);
+  }
+}
 
 // ----------------------------------------------------------------------------
 // symbolic: wave per column, LDS hash of row ids
@@ -643,8 +716,59 @@ struct SymPanelLds {
   int* fine;     // [NFINE_MAX]
   int* pref;     // [BIG_BS + 4]
   int* st;       // [BIG_BS]
-  int* tmp;      // scan scratch
+  int* tmp;      // scan scratch [BIG_BS / WAVE + 4]; tmp[NW + 3]: overflow count
+  int* ovf;      // [SYM_OVF_CAP] rows deferred by hash_claim_bounded
 };
+#ifndef CBG_SYM_OVF  // probes of a symbolic hash insert before it is deferred (0: unbounded)
+#define CBG_SYM_OVF 2
+#endif
+// rows of the symbolic overflow list: what is left of 160 KiB / 4 blocks per
+// CU after the 8192-word bitmap and the staging arrays (the launch keeps 4 blocks)
+constexpr int SYM_OVF_CAP = CBG_SYM_OVF > 0 ? 896 : 0;
+
+// hash_claim with at most NPROBE probes; a row without a slot by then goes to
+// the overflow list (see hash_acc_bounded).  Returns 1 if this call inserted the row.
+template <int NPROBE>
+__device__ __forceinline__ int hash_claim_bounded(int* keys, unsigned h, unsigned mask, int row, int* ocount,
+                                                  int* orow, int cap) {
+  int got = 0;
+  bool done = false;
+#pragma unroll
+  for (int k = 0; k < NPROBE; ++k) {
+    if (!done) {
+      const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
+      if (old == EMPTY_KEY || old == row) {
+        got = old == EMPTY_KEY;
+        done = true;
+      } else {
+        h = (h + 1) & mask;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(!done);
+  if (m) {
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane_id() == leader) base = atomicAdd(ocount, __popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (!done) {
+      const int idx = base + lane_rank(m);
+      if (idx < cap) orow[idx] = row;
+      else got = hash_claim(keys, h, mask, row);
+    }
+  }
+  return got;
+}
+// the deferred rows (after a barrier): this thread's insertions
+template <int NPROBE>
+__device__ __forceinline__ int hash_claim_drain(int* keys, unsigned mask, const int* orow, int n) {
+  int got = 0;
+  for (int i = threadIdx.x; i < n; i += BIG_BS) {
+    const int row = orow[i];
+    got += hash_claim(keys, (((unsigned)row * 0x9E3779B1u) + NPROBE) & mask, mask, row);
+  }
+  return got;
+}
 
 // one (column, panel) pair
 template <class H>
@@ -714,21 +838,32 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
         return;
       }
       int* keys = reinterpret_cast<int*>(bm);
+      int* ocount = tmp + BS / WAVE + 3;
       for (int j = tid; j < T / 4; j += BS)
         reinterpret_cast<int4*>(keys)[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
+      if (tid == 0) *ocount = 0;
       __syncthreads();
       int count = 0;
+      const unsigned mask = (unsigned)(T - 1);
       if (!(c_dbg & 64))
       block_products<BS>(
           pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
           [&](const SegI& g, int u) { return irA[g.off + u]; },
           [&](int row) {
-            count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
+            const unsigned h = ((unsigned)row * 0x9E3779B1u) & mask;
+            if (CBG_SYM_OVF > 0)
+              count += hash_claim_bounded<CBG_SYM_OVF>(keys, h, mask, row, ocount, L.ovf, SYM_OVF_CAP);
+            else
+              count += hash_claim(keys, h, mask, row);
           });
       hook(2);
-      count = wave_sum(count);
       if (tid == 0) fine[0] = 0;
       __syncthreads();
+      if (CBG_SYM_OVF > 0) {
+        const int no = *ocount;
+        if (no > 0) count += hash_claim_drain<CBG_SYM_OVF>(keys, mask, L.ovf, min(no, SYM_OVF_CAP));
+      }
+      count = wave_sum(count);
       if (lane_id() == 0 && count) atomicAdd(&fine[0], count);
       __syncthreads();
       if (tid == 0) {
@@ -912,22 +1047,36 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
     return true;
   }
   int* keys = reinterpret_cast<int*>(L.bm);
+  int* ocount = L.tmp + BS / WAVE + 3;
   for (int j = tid; j < T / 4; j += BS)
     reinterpret_cast<int4*>(keys)[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
-  if (tid == 0) L.fine[0] = 0;
+  if (tid == 0) {
+    L.fine[0] = 0;
+    *ocount = 0;
+  }
   __syncthreads();
   int count = 0;
   const int32_t* __restrict__ irA = a.irA;
   const int* pref = L.pref;
   const int* st = L.st;
+  const unsigned mask = (unsigned)(T - 1);
   if (!(c_dbg & 64))
   block_products<BS>(
       pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
       [&](const SegI& g, int u) { return irA[g.off + u]; },
       [&](int row) {
-        count += hash_claim(keys, ((unsigned)row * 0x9E3779B1u) & (unsigned)(T - 1), (unsigned)(T - 1), row);
+        const unsigned h = ((unsigned)row * 0x9E3779B1u) & mask;
+        if (CBG_SYM_OVF > 0)
+          count += hash_claim_bounded<CBG_SYM_OVF>(keys, h, mask, row, ocount, L.ovf, SYM_OVF_CAP);
+        else
+          count += hash_claim(keys, h, mask, row);
       });
   hook(2);
+  if (CBG_SYM_OVF > 0) {
+    __syncthreads();
+    const int no = *ocount;
+    if (no > 0) count += hash_claim_drain<CBG_SYM_OVF>(keys, mask, L.ovf, min(no, SYM_OVF_CAP));
+  }
   count = wave_sum(count);
   if (lane_id() == 0 && count) atomicAdd(&L.fine[0], count);
   __syncthreads();
@@ -951,7 +1100,15 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
 // grid: RG groups x (columns of the class), group-major, so that the blocks in
 // flight gather A's segments of the same panels, which then stay in L2 /
 // Infinity Cache
-__global__ __launch_bounds__(BIG_BS) void k_sym_panel(SymPanelArgs a) {
+#ifndef CBG_SYM_WPE  // waves per SIMD k_sym_panel is compiled for (0: the compiler's choice)
+#define CBG_SYM_WPE 0
+#endif
+#if CBG_SYM_WPE > 0
+#define CBG_SYM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CBG_SYM_WPE)))
+#else
+#define CBG_SYM_WPE_ATTR
+#endif
+__global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelArgs a) {
   // Persistent blocks stride over the units (group-major order kept); the
   // next unit's dependent loads -- column id, B column range, B rows, A run
   // bounds -- are issued one per stage of the current unit (hook 1 after its
@@ -965,6 +1122,7 @@ __global__ __launch_bounds__(BIG_BS) void k_sym_panel(SymPanelArgs a) {
   L.pref = L.fine + NFINE_MAX;
   L.st = L.pref + BS + 4;
   L.tmp = L.st + BS;
+  L.ovf = L.tmp + BS / WAVE + 4;
   const int tid = threadIdx.x;
   const int g = 1 << a.glog;
   const int RG = (a.R + g - 1) >> a.glog;
@@ -1862,12 +2020,29 @@ struct SlabHashLds {
   static constexpr bool MEMB_ALIAS = CBG_HASH_MEMB_ALIAS && 2 * MEMB * 2 <= IDLE;
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
                                (2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2);
+  // the product loop's overflow list (hash_acc_bounded) lives in boff | cur |
+  // members, which only the emit uses: (value, row) items of 12 B, values first
+  // (boff's offset is a multiple of 8)
+  static constexpr int OFF_BOFF = T * 8 + T * 4 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4;
+  static_assert(OFF_BOFF % 8 == 0, "overflow values are 8-byte aligned");
+  static constexpr int OVF_CAP = ((2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2)) / 12;
 };
+#ifndef CBG_HASH_OVF  // probes a product makes in the product loop before it is deferred (0: unbounded probing)
+#define CBG_HASH_OVF 2
+#endif
 
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
 template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
-__global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
+#ifndef CBG_HASH_WPE  // waves per SIMD the hash-slab kernels are compiled for (0: the compiler's choice)
+#define CBG_HASH_WPE 0
+#endif
+#if CBG_HASH_WPE > 0
+#define CBG_HASH_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CBG_HASH_WPE)))
+#else
+#define CBG_HASH_WPE_ATTR
+#endif
+__global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
                                                       int64_t nA1, const int32_t* __restrict__ irA,
@@ -1894,6 +2069,12 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   int* cur = boff + NB + 4;
   unsigned short* members = L::MEMB_ALIAS ? reinterpret_cast<unsigned short*>(bv) + L::MEMB
                                           : reinterpret_cast<unsigned short*>(cur + NB);
+  constexpr int NPROBE = CBG_HASH_OVF;
+  HashOvf ovf;
+  ovf.count = tmp + NW + 3;
+  ovf.val = reinterpret_cast<double*>(boff);
+  ovf.row = reinterpret_cast<int*>(ovf.val + L::OVF_CAP);
+  ovf.cap = L::OVF_CAP;
   const int tid = threadIdx.x;
   int i = blockIdx.x;
   if (i >= n) return;
@@ -1930,7 +2111,10 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
   fetch1(rec);
   fetch2(rec);
   while (true) {
-    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    if (tid == 0) {
+      tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+      tmp[NW + 3] = 0;  // overflow list
+    }
     const bool pre = staged(rec);
     unsigned long long tmark = wall_clock64();
     if (CBG_VEC_INIT) {  // 16-byte LDS stores (T is a multiple of 256; vals and keys are 16-byte aligned)
@@ -1983,8 +2167,19 @@ __global__ __launch_bounds__(BS) void k_num_slab_hash(const SlabRec* __restrict_
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
           [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
-          [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
+          [&](const RowVal& x) {
+            if (NPROBE > 0) hash_acc_bounded<SR, T, NPROBE>(keys, vals, x.row, x.v, ovf);
+            else hash_acc_t<SR, T>(keys, vals, x.row, x.v);
+          });
       __syncthreads();
+      if (NPROBE > 0) {
+        const int no = *ovf.count;  // uniform
+        if (no > 0) {
+          hash_ovf_drain<SR, T, NPROBE, BS>(keys, vals, ovf, min(no, ovf.cap));
+          __syncthreads();
+          if (tid == 0) *ovf.count = 0;
+        }
+      }
       phase_mark(tmark, 14);
     }
     if (has_next) fetch2(nrec);
@@ -2394,6 +2589,19 @@ static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, D
   df.take(bp.hist);
 }
 
+// bytes the thin columns' expand-sort-reduce holds per product at most: two
+// (key, value) buffers of the radix sort, the unique keys and values, the run
+// flags and positions (64-bit keys)
+constexpr double THIN_BYTES_PER_PRODUCT = 2 * 16 + 16 + 4 + 8;
+static double device_bytes_available() {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0.0;
+  }
+  return (double)fr + (double)pool().bytes_cached();
+}
+
 static int pick_panel_log(int64_t m) {
   int l = FINE_LOG;
   while ((1LL << l) < m && l < PANEL_LOG_MAX) ++l;
@@ -2455,6 +2663,7 @@ struct APrep {
   bool active = false;
   const void* ir = nullptr;
   const void* cp = nullptr;
+  uint64_t ser_ir = 0, ser_cp = 0;  // pool allocation serials of ir / cp (0: not pool memory)
   int64_t nnz = -1, nzc = -1, m = -1, n = -1;
   DBuf<int2> cmap, cmapP;  // cmapP: built by the first call that had big columns
   int plog = -1;
@@ -2542,6 +2751,7 @@ void aprep_end() {
   a.af = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
+  a.ser_ir = a.ser_cp = 0;
   a.nnz = a.nzc = a.m = a.n = -1;
   a.plog = -1;
 }
@@ -2621,8 +2831,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const int64_t nz = B.nzc;
   // A column map (reused across the phases of one MemEfficientSpGEMM)
   APrep& ap = aprep();
-  const bool a_hit = ap.active && ap.ir == A.ir && ap.cp == A.cp && ap.nnz == A.nnz && ap.nzc == A.nzc &&
-                     ap.m == A.m && ap.n == A.n;
+  const uint64_t ser_ir = ap.active ? pool().serial_of(A.ir) : 0, ser_cp = ap.active ? pool().serial_of(A.cp) : 0;
+  const bool a_hit = ap.active && ap.ir == A.ir && ap.cp == A.cp && ap.ser_ir == ser_ir && ap.ser_cp == ser_cp &&
+                     ap.nnz == A.nnz && ap.nzc == A.nzc && ap.m == A.m && ap.n == A.n;
   if (ap.active && !a_hit) {
     ap.cmap.release();
     ap.cmapP.release();
@@ -2630,6 +2841,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.af = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
+    ap.ser_ir = ser_ir;
+    ap.ser_cp = ser_cp;
     ap.nnz = A.nnz;
     ap.nzc = A.nzc;
     ap.m = A.m;
@@ -2668,7 +2881,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
   constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1, THIN_BIN = NSMALL + NGCLS;
   static_assert(THIN_BIN < MAXBINS, "bins");
-  constexpr int64_t THIN_MAX_FLOPS = 1LL << 27;  // int item counts of the sort; ~4 GB of temporaries
   int thin_R = 0;
   {
     static const char* eg = getenv("CBG_GROUPS");
@@ -2692,8 +2904,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     thin_R = (fused && thin_on && bp.R >= 4) ? (int)(bp.R * THIN_RATIO / ratio) : 0;
     bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
-    if (thin_R && sp.hf[THIN_BIN] >= THIN_MAX_FLOPS) {
-      // too many thin products for the sort's temporaries: classify again without
+    if (thin_R && (double)sp.hf[THIN_BIN] * THIN_BYTES_PER_PRODUCT > 0.25 * device_bytes_available()) {
+      // the sort's temporaries (64-bit counts, cbg_sort.hip) would take more than a
+      // quarter of the device memory left: classify again without thin columns
       thin_R = 0;
       bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, 0, THIN_BIN);
       CBG_HIP(hipStreamSynchronize(s));
@@ -2825,7 +3038,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
     const int pwords = 1 << (bp.plog - 5);
     auto lds_of = [&](int hw) {
-      return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4;
+      return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4 +
+             (size_t)SYM_OVF_CAP * 4;
     };
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,

@@ -535,9 +535,11 @@ static int comm_reserve_default() {
   return e ? std::max(0, atoi(e)) : 8;
 }
 
+// one_phase: the cuts are pipeline pieces of ONE phase (fn gets phase 0 for
+// each of them, at its column offset), else piece p is phase p
 static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_t A_gncol, int64_t B_gnrow, int sr,
                        const std::vector<int64_t>& cuts_in, cbg_phase_fn fn, void* user, cbg_tile* C,
-                       bool adaptive = false) {
+                       bool adaptive = false, bool one_phase = false) {
   std::vector<int64_t> cuts = cuts_in;
   int np = (int)cuts.size() - 1;
   const int pr = g->pr, pc = g->pc;
@@ -598,47 +600,61 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   SummaInfo& info = summa_info();
   info = SummaInfo{};
   info.pieces = np;
+  // bytes this rank receives: the remote A tiles of its grid row and the remote
+  // B tiles (all pieces) of its grid column
+  int64_t bytes_a = 0, bytes_b0 = 0, bytes_b1 = 0;
+  for (int s = 0; s < pc; ++s)
+    if (s != g->pcol) bytes_a += tile_bytes(&EA[4 * s]);
+  for (int s = 0; s < pr; ++s)
+    if (s != g->prow)
+      for (int p = 0; p < np; ++p) (p == 0 ? bytes_b0 : bytes_b1) += tile_bytes(eB(s, p));
+  info.bytes_recv = bytes_a + bytes_b0 + bytes_b1;
   double host_ms0 = 0.0;
+  // the A block row's gather and B piece 0 in ONE broadcast group (their
+  // transfers overlap on the row and column links); piece 0's multiply waits
+  // for both
   int local = step([&] {
+    CBG_HIP(hipEventRecord(g->ev_t0, g->comm));
+    const auto h0 = std::chrono::steady_clock::now();
     bcast_group(g, [&] {
       for (int s = 0; s < pc; ++s) {
         cbg_tile& t = s == g->pcol ? const_cast<cbg_tile&>(A) : Ar[s].t;
         bcast_tile(g, COMM_ROW, s, &EA[4 * s], t, s == g->pcol);
       }
+      for (int s = 0; s < pr; ++s)
+        bcast_tile(g, COMM_COL, s, eB(s, 0), s == g->prow ? piece[0] : Bc[0][s].t, s == g->prow);
     });
-    CBG_HIP(hipEventRecord(g->ev_t0, g->comm));
-    const auto h0 = std::chrono::steady_clock::now();
-    post_piece(0);
+    CBG_HIP(hipEventRecord(g->ev_comm, g->comm));
     CBG_HIP(hipEventRecord(g->ev_t1, g->comm));
     host_ms0 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
   });
-  // Adaptive double buffering (PANEL with the default two pieces on a grid):
-  // piece 0 (1/8 of B's columns) has been broadcast; its measured time, scaled
-  // to the rest's bytes, is the transfer that pipelining would hide behind
-  // piece 0's multiply.  An extra piece costs about pipeline_cost_ms() of
-  // compute, so the ranks keep the two pieces only when the hidden transfer
-  // is larger (agreed over the grid: every rank cuts its B tile alike);
-  // otherwise the rest is broadcast at once and the pieces are rejoined into
-  // one multiply.
-  if (adaptive && np == 2 && !local) {
+  // Double buffering (PANEL with the default two pieces on a grid).  On RCCL
+  // grids whose B block column has more than one remote tile (pr >= 3) piece 1
+  // is always broadcast while piece 0 multiplies (rule 1).  Otherwise
+  // (one remote B tile, or the host transport) adaptively: the first group's
+  // measured time (A gather + piece 0, 1/8 of B's columns), scaled to the
+  // rest's bytes, is the transfer that pipelining would hide behind piece 0's
+  // multiply; an extra piece costs about pipeline_cost_ms() of compute, so the
+  // ranks keep the two pieces only when the hidden transfer is larger (rule 2,
+  // agreed over the grid: every rank cuts its B tile alike); otherwise the
+  // rest is broadcast at once and the pieces are rejoined into one multiply
+  // (rule 3).
+  if (np == 2 && adaptive && !g->host_mode && pr >= 3) info.rule = 1;
+  if (adaptive && np == 2 && !local && info.rule == 0) {
     float ms0 = 0.f;
     local = step([&] {
       wait_comm(g);
       if (g->host_mode) ms0 = (float)host_ms0;
       else CBG_HIP(hipEventElapsedTime(&ms0, g->ev_t0, g->ev_t1));
     });
-    int64_t b0 = 0, b1 = 0;
-    for (int s = 0; s < pr; ++s)
-      if (s != g->prow) {
-        b0 += tile_bytes(eB(s, 0));
-        b1 += tile_bytes(eB(s, 1));
-      }
+    const int64_t b0 = bytes_a + bytes_b0, b1 = bytes_b1;
     const double hidden = b0 > 0 ? ms0 * (double)b1 / (double)b0 : 0.0;
     info.bcast_ms_piece0 = ms0;
     info.est_hidden_ms = hidden;
     info.piece_cost_ms = pipeline_cost_ms();
     const int want = hidden > info.piece_cost_ms ? 1 : 0;
     const int dec = agree(g, local ? local : want);  // codes >= 3001 are failures
+    info.rule = dec == 1 ? 2 : 3;
     if (dec > 1) {
       rc = dec;
     } else if (dec == 0) {
@@ -678,8 +694,26 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   const cbg_tile* Ause = &A;
   int cb_rc = 0;
   double panel_ms = 0.0;
+  // exposed communication: the compute stream's wait for each piece's broadcast
+  // (an event before and after the wait; ~0 when the broadcast finished first)
+  std::vector<hipEvent_t> wev;
+  struct EvFree {
+    std::vector<hipEvent_t>& v;
+    ~EvFree() {
+      for (auto e : v) (void)hipEventDestroy(e);
+    }
+  } wev_free{wev};
   for (int p = 0; p < np && !rc; ++p) {
-    local = std::max(local, step([&] { CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0)); }));
+    local = std::max(local, step([&] {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      CBG_HIP(hipEventCreate(&e0));
+      wev.push_back(e0);
+      CBG_HIP(hipEventCreate(&e1));
+      wev.push_back(e1);
+      CBG_HIP(hipEventRecord(e0, cs));
+      CBG_HIP(hipStreamWaitEvent(cs, g->ev_comm, 0));
+      CBG_HIP(hipEventRecord(e1, cs));
+    }));
     if (p + 1 < np) {
       // every rank holds piece p+1's receive buffers before anyone posts it
       local = std::max(local, step([&] { alloc_piece(p + 1); }));
@@ -709,7 +743,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
         Buse = &Bp.t;
       }
       if (fn) {
-        multiply_to_fn(*Ause, *Buse, sr, cs, p, cuts[p], fn, user, cb_rc, panel_ms, 0);
+        multiply_to_fn(*Ause, *Buse, sr, cs, one_phase ? 0 : p, cuts[p], fn, user, cb_rc, panel_ms, 0);
         for (auto& t : Bc[p]) tile_free_device(t.t);
         tile_free_device(own[p].t);
       } else {
@@ -726,6 +760,17 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   }
   if (!rc) rc = agree(g, local);
   if (!rc && adaptive) g_last_panel_ms = panel_ms;
+  if (!rc) {
+    double exposed = 0.0;
+    for (size_t k = 0; k + 1 < wev.size(); k += 2) {
+      float ms = 0.f;
+      if (hipEventSynchronize(wev[k + 1]) == hipSuccess && hipEventElapsedTime(&ms, wev[k], wev[k + 1]) == hipSuccess)
+        exposed += ms;
+      else
+        (void)hipGetLastError();
+    }
+    info.exposed_comm_ms = exposed;
+  }
   if (rc) {
     if (!g->broken) wait_comm(g);  // posted broadcasts complete before their buffers are released
     return rc;
@@ -897,7 +942,7 @@ static int summa_staged(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
 // number of nonempty pieces, whatever the widths of the grid's column blocks.
 static std::vector<int64_t> pipeline_cuts(cbg_grid* g, int64_t n, int64_t n_min) {
   static const char* e = getenv("CBG_PIPELINE");
-  const bool comm = g->pr * g->pc > 1;
+  const bool comm = g->pr > 1;  // B tiles are broadcast only along grid columns of >1 rank
   if (n_min < 16) return {0, n};
   if (!e) return comm ? std::vector<int64_t>{0, n / 8, n} : std::vector<int64_t>{0, n};
   if (!strncmp(e, "1/", 2)) {
@@ -1133,11 +1178,16 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
   check_usable(g);
   arm_fault(g);
   phase_plan() = PhasePlan{};
-  // every local multiply of this call (the plan's sample included on one rank)
-  // multiplies the same A: its column maps are built once
-  APrepScope aprep_scope;
-  const bool automatic = phases <= 0 || mem_gb > 0;
-  if (!automatic && phases >= A_gncol) phases = 1;  // "Resetting to 1" (ParFriends.h:469-473)
+  summa_info() = SummaInfo{};
+  // PANEL: every local multiply of this call (the plan's sample included on
+  // one rank) multiplies the same A, so its column maps are built once.  Not
+  // for STAGED, whose stages multiply different A slices.
+  std::unique_ptr<APrepScope> aprep_scope;
+  if (exec == CBG_EXEC_PANEL) aprep_scope.reset(new APrepScope());
+  // phases == CBG_PHASES_AUTO or a memory budget: the count comes from memory;
+  // otherwise phases < 1 or >= A_gncol is "Resetting to 1" (ParFriends.h:468-473)
+  const bool automatic = phases == CBG_PHASES_AUTO || mem_gb > 0;
+  if (!automatic && (phases < 1 || phases >= A_gncol)) phases = 1;
   int rc = A_gncol != B_gnrow ? CBG_ERR_DIMMISMATCH : CBG_OK;
   int64_t n_min = 0;
   if ((rc = agree_val(g, rc, B.n, &n_min, nullptr))) return rc;
@@ -1159,13 +1209,13 @@ int summa_spgemm_phased(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64
       if (alias) tile_slice_cols(B, 0, B.n, Bcopy.t, cs);
     });
     if ((rc = agree(g, rc))) return rc;
-    summa_info() = SummaInfo{};
     const cbg_tile& Bu = alias ? Bcopy.t : B;
     if (phases == 1) {
       // one phase is Mult_AnXBn_DoubleBuff: B's block column arrives in the
-      // (adaptive) pipeline's pieces, each handed to fn at its column offset
+      // (adaptive) pipeline's pieces, each handed to fn as phase 0 at its column offset
       const bool adaptive = !getenv("CBG_PIPELINE") && g->pr * g->pc > 1;
-      return summa_panel(g, A, Bu, A_gncol, B_gnrow, sr, pipeline_cuts(g, Bu.n, n_min), fn, user, C, adaptive);
+      return summa_panel(g, A, Bu, A_gncol, B_gnrow, sr, pipeline_cuts(g, Bu.n, n_min), fn, user, C, adaptive,
+                         true);
     }
     return summa_panel(g, A, Bu, A_gncol, B_gnrow, sr, cuts, fn, user, C);
   }

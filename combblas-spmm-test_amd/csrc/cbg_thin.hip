@@ -10,14 +10,13 @@
 // R panels, and the R pairs staged 8 x 50 K entries for them (the pair kernels
 // took 1.5 ms of the 7 ms product for 6 % of its flops).  Such columns (flops
 // x 4 < B entries x R) are expanded here instead: every product becomes a
-// (column << rowbits | row, value) pair (32-bit keys when they fit), one radix sort orders them, one
-// reduce-by-key combines equal (column, row) keys with the semiring's add, and
+// (column << rowbits | row, value) pair (32-bit keys when they fit), one radix sort orders them
+// (cbg_sort.hip, 64-bit counts), one reduce-by-key combines equal (column, row) keys with the
+// semiring's add in expansion order, and
 // the unique entries land in the fused columns' temporary, from which the
 // column-order copy (k_copy_fused) moves them to C after the column scan --
 // estimateNNZ_Hash and the hash accumulation of mtSpGEMM.h:362-440, 805-933
 // for these columns, as one sort.
-#include <hipcub/hipcub.hpp>
-
 #include "cbg_device.h"
 #include "cbg_internal.h"
 
@@ -95,37 +94,31 @@ __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* _
   }
 }
 
-template <int SR>
-struct SemAdd {
-  __device__ __forceinline__ double operator()(const double& a, const double& b) const { return Sem<SR>::add(a, b); }
-};
-
 // unique keys -> rows in the temporary, and the first unique of every column
 template <typename K>
-__global__ void k_thin_rows(const K* __restrict__ uk, const int* __restrict__ nruns, int rowbits,
-                            int32_t* __restrict__ tir, int64_t* __restrict__ first) {
+__global__ void k_thin_rows(const K* __restrict__ uk, int64_t nruns, int rowbits, int32_t* __restrict__ tir,
+                            int64_t* __restrict__ first) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= *nruns) return;
+  if (i >= nruns) return;
   const K k = uk[i];
   tir[i] = (int32_t)(k & (((K)1 << rowbits) - 1));
   if (i == 0 || (uk[i - 1] >> rowbits) != (k >> rowbits)) first[k >> rowbits] = i;
 }
 
 __global__ void k_thin_slots(const int32_t* __restrict__ perm, int n, const int64_t* __restrict__ first,
-                             const int* __restrict__ nruns, int64_t base, int32_t* __restrict__ cnt,
-                             int64_t* __restrict__ tslot) {
+                             int64_t nruns, int64_t base, int32_t* __restrict__ cnt, int64_t* __restrict__ tslot) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int col = perm[i];
-  const int64_t f0 = first[i], f1 = i + 1 < n ? first[i + 1] : (int64_t)*nruns;
+  const int64_t f0 = first[i], f1 = i + 1 < n ? first[i + 1] : nruns;
   cnt[col] = (int32_t)(f1 - f0);
   tslot[col] = base + f0;
 }
 
-template <typename K, int SR>
+template <typename K>
 void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-               const int2* cmap, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base, int rowbits,
-               int colbits, hipStream_t s, DeferredFree& df) {
+               const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base,
+               int rowbits, int colbits, hipStream_t s, DeferredFree& df) {
   DBuf<int64_t> nbe(n + 1), eoff(n + 1), first(n);
   hipLaunchKernelGGL(k_thin_sizes, dim3((n + 255) / 256), dim3(256), 0, s, perm, n, B.cp, nbe.p);
   exclusive_scan_i64(nbe.p, eoff.p, n, s, &df);
@@ -134,25 +127,20 @@ void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_t
   hipLaunchKernelGGL(k_thin_entries, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, perm, n, eoff.p, E, B.cp,
                      B.ir, cmap, ecol.p, epos.p, elen.p);
   exclusive_scan_i64(elen.p, poff.p, E, s, &df);
-  DBuf<K> k0(fthin), k1(fthin);
-  DBuf<double> v0(fthin), v1(fthin);
-  hipLaunchKernelGGL((k_thin_expand<K, SR>), dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, ecol.p, epos.p,
-                     poff.p, B.ir, B.val, cmap, A.ir, A.val, rowbits, k0.p, v0.p);
+  DBuf<K> k0(fthin), uk(fthin);
+  DBuf<double> v0(fthin);
+  if (semiring == CBG_MIN_PLUS)
+    hipLaunchKernelGGL((k_thin_expand<K, 1>), dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, ecol.p, epos.p,
+                       poff.p, B.ir, B.val, cmap, A.ir, A.val, rowbits, k0.p, v0.p);
+  else
+    hipLaunchKernelGGL((k_thin_expand<K, 0>), dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, ecol.p, epos.p,
+                       poff.p, B.ir, B.val, cmap, A.ir, A.val, rowbits, k0.p, v0.p);
   const int end_bit = rowbits + colbits;
-  size_t bytes = 0;
-  CBG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k0.p, k1.p, v0.p, v1.p, (int)fthin, 0, end_bit, s));
-  DBuf<char> tmp(bytes);
-  CBG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, bytes, k0.p, k1.p, v0.p, v1.p, (int)fthin, 0, end_bit, s));
-  DBuf<int> nruns(1);
-  size_t bytes2 = 0;
-  CBG_HIP(hipcub::DeviceReduce::ReduceByKey(nullptr, bytes2, k1.p, k0.p, v1.p, tval + base, nruns.p, SemAdd<SR>(),
-                                            (int)fthin, s));
-  DBuf<char> tmp2(bytes2);
-  CBG_HIP(hipcub::DeviceReduce::ReduceByKey(tmp2.p, bytes2, k1.p, k0.p, v1.p, tval + base, nruns.p, SemAdd<SR>(),
-                                            (int)fthin, s));
-  hipLaunchKernelGGL(k_thin_rows<K>, dim3((unsigned)((fthin + 255) / 256)), dim3(256), 0, s, k0.p, nruns.p, rowbits,
+  radix_sort_pairs<K>(k0, v0, fthin, end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1, s);
+  const int64_t nruns = reduce_by_key<K>(k0.p, v0.p, fthin, semiring, uk.p, tval + base, s);
+  hipLaunchKernelGGL(k_thin_rows<K>, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, s, uk.p, nruns, rowbits,
                      tir + base, first.p);
-  hipLaunchKernelGGL(k_thin_slots, dim3((n + 255) / 256), dim3(256), 0, s, perm, n, first.p, nruns.p, base, cnt,
+  hipLaunchKernelGGL(k_thin_slots, dim3((n + 255) / 256), dim3(256), 0, s, perm, n, first.p, nruns, base, cnt,
                      tslot);
   df.take(nbe);
   df.take(eoff);
@@ -162,27 +150,22 @@ void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_t
   df.take(elen);
   df.take(poff);
   df.take(k0);
-  df.take(k1);
+  df.take(uk);
   df.take(v0);
-  df.take(v1);
-  df.take(tmp);
-  df.take(nruns);
-  df.take(tmp2);
 }
 
-template <int SR>
-void thin_sr(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-             const int2* cmap, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base, hipStream_t s,
-             DeferredFree& df) {
+void thin_any(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
+              const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base,
+              hipStream_t s, DeferredFree& df) {
   int rowbits = 1, colbits = 1;
   while ((1LL << rowbits) < A.m) ++rowbits;
   while ((1LL << colbits) < (int64_t)n) ++colbits;
   // (column, row) keys in 32 bits when they fit: fewer radix passes, half the key traffic
   if (rowbits + colbits <= 32)
-    thin_impl<uint32_t, SR>(perm, n, E, fthin, A, B, cmap, cnt, tslot, tir, tval, base, rowbits, colbits, s, df);
+    thin_impl<uint32_t>(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, rowbits, colbits, s, df);
   else
-    thin_impl<unsigned long long, SR>(perm, n, E, fthin, A, B, cmap, cnt, tslot, tir, tval, base, rowbits, colbits,
-                                      s, df);
+    thin_impl<unsigned long long>(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, rowbits,
+                                  colbits, s, df);
 }
 
 }  // namespace
@@ -191,10 +174,7 @@ void thin_columns(const int32_t* perm, int n, int64_t E, int64_t fthin, const cb
                   const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval,
                   int64_t base, hipStream_t s, DeferredFree& df) {
   if (n <= 0 || fthin <= 0 || E <= 0) return;
-  if (semiring == CBG_MIN_PLUS)
-    thin_sr<1>(perm, n, E, fthin, A, B, cmap, cnt, tslot, tir, tval, base, s, df);
-  else
-    thin_sr<0>(perm, n, E, fthin, A, B, cmap, cnt, tslot, tir, tval, base, s, df);
+  thin_any(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, s, df);
 }
 
 // the thin columns' entries -> C: a block per column (k_copy_fused's few

@@ -43,6 +43,7 @@ void* DevicePool::alloc(size_t bytes) {
       free_.erase(it);
       cached_ -= sz;
       live_[p] = sz;
+      serial_[p] = ++next_serial_;
       in_use_ += sz;
       return p;
     }
@@ -67,8 +68,25 @@ void* DevicePool::alloc(size_t bytes) {
   }
   std::lock_guard<std::mutex> lk(mu_);
   live_[p] = rb;
+  serial_[p] = ++next_serial_;
   in_use_ += rb;
   return p;
+}
+
+uint64_t DevicePool::serial_of(const void* p) {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = serial_.upper_bound(const_cast<void*>(p));
+  if (it == serial_.begin()) return 0;
+  --it;
+  size_t size = 0;
+  auto l = live_.find(it->first);
+  if (l != live_.end()) {
+    size = l->second;
+  } else {
+    auto g = grow_.find(it->first);
+    if (g != grow_.end()) size = g->second.reserved;
+  }
+  return static_cast<const char*>(p) < static_cast<const char*>(it->first) + size ? it->second : 0;
 }
 
 bool DevicePool::release_largest_cached() {
@@ -84,6 +102,7 @@ bool DevicePool::release_largest_cached() {
 void DevicePool::free(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(mu_);
+  serial_.erase(p);
   auto it = live_.find(p);
   if (it == live_.end()) {
     auto g = grow_.find(p);
@@ -142,6 +161,7 @@ void* DevicePool::reserve_growable(size_t max_bytes) {
       in_use_ += best->second.mapped;
       grow_.emplace(p, std::move(best->second));
       grow_cache_.erase(best);
+      serial_[p] = ++next_serial_;
       return p;
     }
   }
@@ -149,6 +169,7 @@ void* DevicePool::reserve_growable(size_t max_bytes) {
   CBG_HIP(hipMemAddressReserve(&p, r, g, nullptr, 0));
   std::lock_guard<std::mutex> lk(mu_);
   grow_[p].reserved = r;
+  serial_[p] = ++next_serial_;
   return p;
 }
 

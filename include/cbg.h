@@ -125,11 +125,19 @@ int cbg_tile_transpose(const cbg_tile* t, cbg_tile* out);
 enum { CBG_DIM_COLUMN = 0, CBG_DIM_ROW = 1 };
 enum { CBG_OP_MULTIPLIES = 0, CBG_OP_PLUS = 1, CBG_OP_MIN = 2, CBG_OP_MAX = 3 };
 int cbg_tile_dim_apply(cbg_tile* t, int dim, const double* vec, int op);
-/* Restriction operator of the Galerkin driver (mfiles/genrestrict.m: n x n/order,
- * about n nonzeros, values in (0,1]): T(i, c(i)) = v(i) for every fine row i with
- * c(i), v(i) from a counter-based hash of (seed, i), so every grid shape sees the
- * same global T.  Tile (prow,pcol) of the pr x pc block distribution. */
+/* Restriction operator of the Galerkin driver (mfiles/genrestrict.m:11,
+ * sprand(n, n/order, order/n)): n x n/order, Poisson(1) nonzeros per fine row
+ * (~37 % of the rows empty) in uniform coarse columns (Poisson(order) per
+ * column), values in (0,1]; counts, columns and values from a counter-based
+ * hash of (seed, row), a column drawn twice in a row summed, so every grid
+ * shape sees the same global T.  Tile (prow,pcol) of the pr x pc block
+ * distribution. */
 int cbg_restriction_tile(int scale, int order, uint64_t seed, int pr, int pc, int prow, int pcol, cbg_tile* out);
+/* Test inputs with random values: every nonzero (i, j) of the
+ * tile, at global row i + row_off and column j + col_off, gets a value
+ * U[-1, 1) from a counter hash of (seed, column, row) (exact in double; the
+ * structure is kept).  In place. */
+int cbg_tile_random_values(cbg_tile* t, uint64_t seed, int64_t row_off, int64_t col_off);
 
 /* ---------------- generator ---------------- */
 /* Graph500 Kronecker R-MAT as DistEdgeList::GenGraph500Data(packed, scrambled)
@@ -163,6 +171,12 @@ int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);
  * (0.04) x the previous such call's local multiply ms); pipelined when the
  * hidden ms exceed the cost on some rank */
 int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms, double* piece_cost_ms);
+/* ... and its communication: the double-buffering rule applied (0 one piece,
+ * 1 pipelined because the B block column has > 1 remote tile on an RCCL grid,
+ * 2 adaptive and pipelined, 3 adaptive and rejoined), the bytes of the remote
+ * A and B tiles this rank received, and the exposed communication: the summed
+ * ms the compute stream waited for broadcasts (HIP events around each wait) */
+int cbg_last_summa_comm(int* rule, int64_t* bytes_recv, double* exposed_comm_ms);
 
 /* ---------------- 2D SUMMA over RCCL ---------------- */
 typedef struct cbg_grid cbg_grid;
@@ -219,25 +233,29 @@ int cbg_summa_spgemm(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_loc
  *               and freed after the call (C streamed when it does not fit HBM;
  *               C_local may be NULL).  fn runs on every rank between the
  *               collectives; a nonzero return is reported after all phases.
- * phases >= A_gncol is reset to 1 (ParFriends.h:469-473); phases <= 0 picks the
- * count from device memory (see cbg_summa_spgemm_memeff).  Every rank needs
- * B_local->n >= phases (CBG_ERR_INVALIDPARAMS otherwise, collectively).  With fn,
- * a phase whose C does not fit the device after all is computed as column
- * halves of its B piece (each handed to fn with the same phase index and its
- * own col_offset). */
+ *               fn may be called SEVERAL times per phase, each time with a
+ *               column piece of that phase's C at its own col_offset: with
+ *               phases == 1 and EXEC_PANEL the SUMMA's pipeline pieces are
+ *               handed over one by one (phase 0 each), and with EXEC_PANEL a
+ *               phase whose C does not fit the device after all is computed as
+ *               column halves of its B piece (same phase index).  With
+ *               EXEC_STAGED such a phase fails with CBG_ERR_OOM.
+ * phases < 1 or >= A_gncol is reset to 1 (ParFriends.h:468-473).  Every rank needs
+ * B_local->n >= phases (CBG_ERR_INVALIDPARAMS otherwise, collectively). */
 typedef int (*cbg_phase_fn)(void* user, int phase, int64_t col_offset, const cbg_tile* C_phase);
 int cbg_summa_spgemm_phased(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
                             int64_t B_gnrow, int semiring, int algo, int exec, int phases, cbg_phase_fn fn,
                             void* user, cbg_tile* C_local);
 /* The same with MemEfficientSpGEMM's perProcessMemory (GB, ParFriends.h:482-535):
- * when per_process_memory_gb > 0 (or phases <= 0) the phase count comes from
- * memory: the flops of this rank's product (from the column counts of A's tiles
+ * when per_process_memory_gb > 0, or phases == CBG_PHASES_AUTO (this library's
+ * extension: the device's free memory), the phase count comes from memory: the flops of this rank's product (from the column counts of A's tiles
  * and the row counts of B's tiles, allgathered along the grid row / column), an
  * nnz(C) estimate (flops, times the compression of an exact symbolic of a sample
  * of the product when the flops bound asks for more than one phase), and 60 % of
  * the memory left after the tiles the SUMMA gathers -- perProcessMemory, or the device's free memory when it is 0;
  * the maximum over the grid.  If that memory is already taken by the inputs the
  * given phases are kept, like the reference. */
+#define CBG_PHASES_AUTO (-1)
 int cbg_summa_spgemm_memeff(cbg_grid* g, const cbg_tile* A_local, const cbg_tile* B_local, int64_t A_gncol,
                             int64_t B_gnrow, int semiring, int algo, int exec, int phases,
                             int64_t per_process_memory_gb, cbg_phase_fn fn, void* user, cbg_tile* C_local);

@@ -208,20 +208,52 @@ def _mix_np(z):
         return z ^ (z >> np.uint64(31))
 
 
+POISSON1_CDF = np.array([0.36787944117144233, 0.7357588823428847, 0.9196986029286058, 0.9810118431238463,
+                         0.9963401531726563, 0.9994058151824183, 0.999916758850712, 0.9999897508033253,
+                         0.999998874797402, 0.9999998885745216, 0.9999999899522336, 0.9999999991683892])
+
+
 def restriction_host(scale, order=2, seed=0x5EED):
-    """global restriction operator of cbg_restriction_tile (csrc/cbg_ops.hip k_restrict_keys)."""
+    """global restriction operator of cbg_restriction_tile (csrc/cbg_ops.hip k_restrict_count /
+    k_restrict_fill): genrestrict.m:11's sprand(n, n/order, order/n) shape -- Poisson(1)
+    nonzeros per fine row (count by inversion of the CDF table), uniform coarse columns,
+    values in (0, 1], a column drawn twice in one row summed."""
     n = 1 << scale
     nc = n // order
     i = np.arange(n, dtype=np.uint64)
     with np.errstate(over="ignore"):
         h = _mix_np(np.uint64(seed) ^ (i * np.uint64(0xD1B54A32D192ED03)))
-    c = (h % np.uint64(nc)).astype(np.int64)
-    v = ((_mix_np(h) >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * (1.0 / 9007199254740992.0)
-    order_ = np.lexsort((np.arange(n), c))
-    rows, cols, vals = np.arange(n)[order_], c[order_], v[order_]
-    jc, start = np.unique(cols, return_index=True)
-    return dict(m=n, n=nc, cp=np.append(start, n).astype(np.int64), jc=jc.astype(np.int32),
-                ir=rows.astype(np.int32), val=vals)
+        u = (_mix_np(h ^ np.uint64(0x5851F42D4C957F2D)) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+        k = np.searchsorted(POISSON1_CDF, u, side="right")
+        rows = np.repeat(np.arange(n, dtype=np.int64), k)
+        starts = np.repeat(np.cumsum(k) - k, k)
+        j = np.arange(len(rows), dtype=np.int64) - starts
+        hj = _mix_np(h[rows] + (j + 1).astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+    cols = (hj % np.uint64(nc)).astype(np.int64)
+    vals = ((_mix_np(hj) >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    o = np.lexsort((j, rows, cols))
+    r, c, v = rows[o], cols[o], vals[o]
+    head = np.ones(len(r), bool)
+    head[1:] = (r[1:] != r[:-1]) | (c[1:] != c[:-1])
+    run = np.cumsum(head) - 1
+    uv = np.zeros(int(head.sum()))
+    np.add.at(uv, run, v)  # duplicates summed in draw order
+    ur, uc = r[head], c[head]
+    jc, start = np.unique(uc, return_index=True)
+    return dict(m=n, n=nc, cp=np.append(start, len(ur)).astype(np.int64), jc=jc.astype(np.int32),
+                ir=ur.astype(np.int32), val=uv)
+
+
+def random_values_host(t, seed=0x5EEDF00D, roff=0, coff=0):
+    """Tile.set_random_values (csrc/cbg_ops.hip random_value) on a host tile: a copy with
+    every (row, col) value = U[-1, 1) from mix(((col << 32) | row) ^ seed * K)."""
+    col = tile_cols(t).astype(np.uint64) + np.uint64(coff)
+    row = t["ir"].astype(np.uint64) + np.uint64(roff)
+    with np.errstate(over="ignore"):
+        z = _mix_np(((col << np.uint64(32)) | row) ^ (np.uint64(seed) * np.uint64(0xD1B54A32D192ED03)))
+    u = dict(t)
+    u["val"] = (z >> np.uint64(11)).astype(np.float64) * (1.0 / 4503599627370496.0) - 1.0
+    return u
 
 
 def transpose_host(d):

@@ -157,6 +157,25 @@ def main():
             if rank == 0:
                 print(algo, ex, "OK" if good else f"BAD {tot} unsorted={uns} vs {gd}", flush=True)
             ok = ok and good
+        # the grid branch of MemEfficientSpGEMM's phase planner (ParFriends.h:482-535):
+        # perProcessMemory = 1 GB asks for several phases on every rank of this
+        # grid (C = 5.1 GB); the count is agreed (equal on every rank), the plan's
+        # flops are this rank's product flops, and the streamed phases add up to
+        # the reference's digest
+        parts = []
+        cbg.MemEfficientSpGEMM(Ad, Bd, cbg.PHASES_AUTO, perProcessMemory=1,
+                               on_phase=lambda ph, off, t: parts.append(t.digest(r0, c0 + off)))
+        plan, st = cbg.phase_plan(), cbg.last_stats()
+        mine = add_digests(parts)
+        mine["phases"], mine["flops_ok"] = plan["phases"], plan["flops"] == st["flops"]
+        alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(mine))))]
+        tot = add_digests(alld)
+        good = (tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and tot["hv"] == gd["hv"]
+                and len({x["phases"] for x in alld}) == 1 and alld[0]["phases"] > 1 and all(x["flops_ok"] for x in alld)
+                and plan["automatic"] == 1)
+        if rank == 0:
+            print("planned phases", alld[0]["phases"], "OK" if good else f"BAD {alld} vs {gd}", flush=True)
+        ok = ok and good
         grid.destroy()
         dist.barrier()
         if rank == 0 and ok:
@@ -480,6 +499,18 @@ def main():
     good = same and tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"]
     if rank == 0:
         print("phased", "OK" if good else f"BAD same={same} {tot} vs {gd}", flush=True)
+    ok = ok and good
+    # phases = 1 with a consumer: the SUMMA's pipeline pieces (2 on a grid when the
+    # adaptive pipeline keeps them) are all handed over as phase 0, at their offsets
+    seen = []
+    cbg.MemEfficientSpGEMM(Ad, Bd, 1, on_phase=lambda ph, off, t: seen.append((ph, t.digest(r0, c0 + off))))
+    mine = add_digests([d for _, d in seen])
+    mine["ph"] = sorted({ph for ph, _ in seen})
+    alld = [pickle.loads(b) for b in _chunks(hc.allgather(0, _pad(pickle.dumps(mine))))]
+    tot = add_digests(alld)
+    good = tot["nnz"] == gd["nnz"] and tot["hs"] == gd["hs"] and all(x["ph"] == [0] for x in alld)
+    if rank == 0:
+        print("phases=1 consumer pieces", len(seen), "OK" if good else f"BAD {alld}", flush=True)
     ok = ok and good
     C1.tile.free()
     Cp.tile.free()

@@ -455,11 +455,11 @@ def _add(ds):
                 unsorted=sum(d["unsorted"] for d in ds))
 
 
-def _tile_digests(cbg, scale, pr, pc, phases=0):
+def _tile_digests(cbg, scale, pr, pc, phases=-1):
     """every rank's C tile of scale-`scale` A*A on a pr x pc grid, computed on this one
     GPU the way the rank computes it (its A block row times its B block column,
     generated on device as the (pr x 1) / (1 x pc) tiles), streamed in B-column
-    phases (0: picked from device memory, as the bench does); each phase digested at
+    phases (-1 = PHASES_AUTO: picked from device memory, as the bench does); each phase digested at
     its global offsets (row block start, column block start + phase offset), so the
     sum is the digest of the whole C.  Returns (summed digest, phase plans)."""
     from combblas_spmm_test_amd import block_range
@@ -516,6 +516,47 @@ def test_rank_tiles_scale24_2x4(cbg):
         assert (d["nnz"], d["hs"], d["hv"]) == (g["nnz"], g["hs"], g["hv"])
 
 
+def test_rank_tiles_scale24_2x4_values(cbg):
+    """Config 4's 2x4 rank tiles with their VALUES pinned on a strided sample of C: column
+    pieces p = 16k of 512 (8 in each of the grid's 4 block columns; digests of the CPU
+    oracle, tests/golden/oracle_large.json s24_ef16_pieces).  For every sampled piece
+    the ranks (r, c) whose block column holds it multiply their A block row (2^23 x 2^24
+    rows/columns: R = 32 row panels) by that piece of their B block column -- the work
+    their PANEL SUMMA does for those columns after the broadcasts; the two row blocks'
+    digests at their global offsets add up to the oracle's digest of the piece
+    (structure and values bit-exact, rows sorted)."""
+    from combblas_spmm_test_amd import block_range
+    g = _oracle_large("s24_ef16_pieces")
+    n = 1 << 24
+    w = n // g["pieces"]
+    sample = sorted(p for p in (int(k) for k in g["digests"]) if p % 16 == 0)
+    assert len(sample) >= 32 and {p * w * 4 // n for p in sample} == {0, 1, 2, 3}
+    got = {p: [] for p in sample}
+    for c in range(4):
+        Bc = cbg.rmat_tile(24, 16, grid=(1, 4), pos=(0, c))
+        c0 = block_range(n, 4, c)[0]
+        mine = [p for p in sample if c0 <= p * w < c0 + Bc.n]
+        for r in range(2):
+            Ar = cbg.rmat_tile(24, 16, grid=(2, 1), pos=(r, 0))
+            r0 = block_range(n, 2, r)[0]
+            for p in mine:
+                lo = p * w - c0
+                left, right = Bc.split_cols(lo + w)
+                right.free()
+                low, Bp = left.split_cols(lo)
+                low.free()
+                left.free()
+                C = cbg.LocalHybridSpGEMM(Ar, Bp)
+                got[p].append(C.digest(r0, p * w))
+                C.free()
+                Bp.free()
+            Ar.free()
+        Bc.free()
+    for p in sample:
+        d, ref = _add(got[p]), g["digests"][str(p)]
+        assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (ref["nnz"], ref["hs"], ref["hv"], 0), (p, d, ref)
+
+
 def _oracle_all():
     import json
     import os
@@ -525,16 +566,18 @@ def _oracle_all():
 
 def test_auto_phases_plan(cbg):
     """MemEfficientSpGEMM's memory-driven phase count (ParFriends.h:482-535): the plan's
-    flops are the product's exact flops (from the tiles' count vectors); phases = 0 on
+    flops are the product's exact flops (from the tiles' count vectors); PHASES_AUTO on
     scale 18 (C = 5 GB) runs one phase; perProcessMemory = 2 GB forces several; the
-    streamed phases add up to the reference's digest either way."""
+    streamed phases add up to the reference's digest either way.  phases = 0 without a
+    memory budget is the reference's "Resetting to 1" (ParFriends.h:468-473)."""
     grid = _self_grid_1x1(cbg)
     A = cbg.SpParMat.rmat(grid, 18)
     B = cbg.SpParMat.rmat(grid, 18)
     gd = G["rmat"]["s18_ef16"]["C_local_plus"]
     for kw in ({}, {"perProcessMemory": 2}):
         parts = []
-        cbg.MemEfficientSpGEMM(A, B, 0, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)), **kw)
+        cbg.MemEfficientSpGEMM(A, B, cbg.PHASES_AUTO, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)),
+                               **kw)
         plan, st = cbg.phase_plan(), cbg.last_stats()
         d = _add(parts)
         assert (d["nnz"], d["hs"], d["hv"], d["unsorted"]) == (gd["nnz"], gd["hs"], gd["hv"], 0), kw
@@ -548,6 +591,12 @@ def test_auto_phases_plan(cbg):
         else:
             # the flops bound (12 B x 1.1e9) fits the device: one phase, no sample taken
             assert plan["phases"] == 1 and plan["nnz_est"] == plan["flops"], plan
+    for ph in (0, -3):  # the reference's reset to 1, not a memory plan
+        parts = []
+        cbg.MemEfficientSpGEMM(A, B, ph, on_phase=lambda p, off, t: parts.append((p, t.digest(0, off))))
+        plan = cbg.phase_plan()
+        assert plan["phases"] == 1 and not plan["automatic"] and {p for p, _ in parts} == {0}, plan
+        assert _add([d for _, d in parts])["hs"] == gd["hs"]
     A.tile.free()
     B.tile.free()
     grid.destroy()
@@ -1003,6 +1052,64 @@ def test_local_digest_large_vs_oracle(cbg, scale, sr):
         assert d["nnz"] == sym["nnzC"]
 
 
+def _cols_host(t, keep):
+    """the columns j of host tile t with keep(j) (ids kept, same n)"""
+    sel = np.flatnonzero(keep(t["jc"].astype(np.int64)))
+    cnt = np.diff(t["cp"])[sel]
+    starts = t["cp"][sel]
+    idx = np.repeat(starts - np.concatenate([[0], np.cumsum(cnt)[:-1]]), cnt) + np.arange(int(cnt.sum()))
+    return dict(m=t["m"], n=t["n"], cp=np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64),
+                jc=t["jc"][sel].copy(), ir=t["ir"][idx], val=t["val"][idx])
+
+
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_random_values_scale20_vs_oracle(cbg, sr):
+    """SURVEY 8(d)'s random-valued variant at multi-panel scale: the R-MAT scale-20
+    structure (R = 4 row panels: bitmap and hash (column, panel) pairs, panel groups,
+    multi-slab pairs) with values U[-1, 1) from a hash of (row, col), which are not f32
+    (the slab kernels' f64-value instantiations run); B = every 16th column of A.
+    Entry by entry against the CPU oracle: plus-times within 1e-12 (|A||B|)_ij, min-plus
+    exact.  The device values equal the host restatement bit for bit."""
+    from helpers import random_values_host
+    A = cbg.rmat_tile(20, 16).set_random_values()
+    Ah = A.to_host()
+    np.testing.assert_array_equal(Ah["val"], random_values_host(Ah)["val"])
+    Bh = _cols_host(Ah, lambda j: j % 16 == 0)
+    B = cbg.Tile.from_dict(Bh)
+    C = cbg.LocalHybridSpGEMM(A, B, sr)
+    st = cbg.last_stats()
+    assert st["n_big"] > 0 and st["n_slabs"] > 0, st
+    Ch = C.to_host()
+    C.free()
+    ref = oracle_local(Ah, Bh, sr)
+    if sr == "plus":
+        assert_tiles_equal(Ch, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+    else:
+        assert_tiles_equal(Ch, ref)
+    A.free()
+    B.free()
+
+
+def test_random_values_scale24_piece_vs_oracle(cbg):
+    """The same at scale 24 (R = 64 row panels, panel groups of up to 64 panels, hash
+    slabs spanning up to 2^24 rows): C's B-column piece 0 of 512 (B = A's columns
+    [0, n/512)) with random values, entry by entry within 1e-12 (|A||B|)_ij."""
+    n = 1 << 24
+    A = cbg.rmat_tile(24, 16).set_random_values()
+    left, right = A.split_cols(n // 512)
+    right.free()
+    C = cbg.LocalHybridSpGEMM(A, left)
+    Ch = C.to_host()
+    C.free()
+    Ah, Bh = A.to_host(), left.to_host()
+    A.free()
+    left.free()
+    ref = oracle_local(Ah, Bh)
+    bound = oracle_local(abs_tile(Ah), abs_tile(Bh))["val"]
+    assert len(Ch["ir"]) == _oracle_large("s24_ef16_pieces")["digests"]["0"]["nnz"]
+    assert_tiles_equal(Ch, ref, rtol=RTOL, bound=bound)
+
+
 def test_local_scale24_column_pieces_vs_oracle(cbg):
     """Scale 24 (2^24 rows: R = 64 row panels, groups of up to 64 panels) pinned
     against the CPU oracle on a sample of C: column pieces p of 512 (B = A's
@@ -1051,10 +1158,10 @@ def test_local_scale22_ef8_resident(cbg):
     assert d["nnz"] == sym["nnzC"] and st["flops"] == sym["flops"]
 
 
-@pytest.mark.parametrize("sr,phases", [("plus", 0), ("plus", 3), ("plus", 4), ("minplus", 0)])
+@pytest.mark.parametrize("sr,phases", [("plus", -1), ("plus", 3), ("plus", 4), ("minplus", -1)])
 def test_phased_scale22_vs_oracle(cbg, sr, phases):
     """The bench's configuration: R-MAT scale-22 A*A as MemEfficientSpGEMM on one GPU with
-    the phase count picked from device memory (phases=0, what bench.py times: 3 phases),
+    the phase count picked from device memory (PHASES_AUTO, what bench.py times: 2 phases),
     and 3 and 4 phases forced; each phase's C digested on the device as it is
     streamed; the sum equals the oracle's digest of the whole C (24.8 G nonzeros,
     tests/golden/oracle_large.json; min-plus too) and nnz the reference's symbolic total."""
@@ -1069,8 +1176,8 @@ def test_phased_scale22_vs_oracle(cbg, sr, phases):
     parts = []
     cbg.MemEfficientSpGEMM(A, B, phases, sr=sr, on_phase=lambda ph, off, t: parts.append(t.digest(0, off)))
     plan = cbg.phase_plan()
-    assert plan["phases"] == (phases or plan["phases"]) and plan["automatic"] == (phases == 0)
-    if phases == 0:
+    assert plan["phases"] == (phases if phases > 0 else plan["phases"]) and plan["automatic"] == (phases < 0)
+    if phases < 0:
         assert 2 <= plan["phases"] <= 4 and plan["oom_splits"] == 0, plan
     hs = "%016x" % (sum(int(d["hs"], 16) for d in parts) % (1 << 64))
     hv = "%016x" % (sum(int(d["hv"], 16) for d in parts) % (1 << 64))

@@ -7,6 +7,8 @@ reference-generated golden vectors; no GPU is used.
 
   nice -n 19 python tools/oracle_digest_pieces.py --scale 24 --pieces 256 --threads 6 \
       --state /tmp/s24_pieces.jsonl
+  # a strided sample (config 4's 2x4 grid: 128 pieces per grid column, 8 from each)
+  python tools/oracle_digest_pieces.py --scale 24 --pieces 512 --only 0:512:16 --state ...
 
 Prints the summed digest (tools/check_scale.py's definition: hs, hv mod 2^64,
 vsum, unsorted) when all pieces are done.
@@ -30,7 +32,9 @@ def main():
     p.add_argument("--pieces", type=int, default=64)
     p.add_argument("--threads", type=int, default=6)
     p.add_argument("--state", required=True)
+    p.add_argument("--only", default=None, help="start:stop:step of the pieces to compute (default: all)")
     a = p.parse_args()
+    want = range(a.pieces) if a.only is None else range(*[int(x) for x in a.only.split(":")])
     from check_scale import add, chunked_digest
     from helpers import oracle_local, oracle_rmat
     import numpy as np
@@ -46,7 +50,7 @@ def main():
     print(json.dumps({"A_nnz": int(len(A["ir"])), "gen_s": round(time.time() - t0, 1)}), flush=True)
     n = A["n"]
     cp, jc = A["cp"], A["jc"]
-    for ph in range(a.pieces):
+    for ph in want:
         if ph in done:
             continue
         c0, c1 = ph * (n // a.pieces), (n if ph == a.pieces - 1 else (ph + 1) * (n // a.pieces))
@@ -62,6 +66,10 @@ def main():
             f.write(json.dumps(d) + "\n")
         done[ph] = d
         print(json.dumps(d), flush=True)
+    if a.only is not None:
+        print(json.dumps({"scale": a.scale, "ef": a.ef, "sr": a.sr, "pieces": a.pieces,
+                          "digests": {str(k): done[k] for k in want}}), flush=True)
+        return
     tot = add([done[k] for k in range(a.pieces)])
     tot["unsorted"] = sum(done[k]["unsorted"] for k in range(a.pieces))
     print(json.dumps({"scale": a.scale, "ef": a.ef, "sr": a.sr, "pieces": a.pieces, "digest": tot}), flush=True)
