@@ -378,78 +378,9 @@ __device__ __forceinline__ void hash_acc_t(int* keys, double* vals, int row, dou
     h = h + 1 == T ? 0u : h + 1;
   }
 }
-// the same from probe position h on (an overflow item resumes where it stopped)
-template <int SR, int T>
-__device__ __forceinline__ void hash_acc_from(int* keys, double* vals, int row, double v, unsigned h) {
-  while (true) {
-    const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-    if (old == EMPTY_KEY || old == row) {
-      Sem<SR>::lds_acc(&vals[h], v);
-      return;
-    }
-    h = h + 1 == T ? 0u : h + 1;
-  }
-}
-
-// Bounded probing with a block overflow list.  A wave's linear-probe loop
-// runs until its slowest lane has found a slot: at load 2/3 that is ~10 CAS
-// wave-instructions per 64 products (rocprofv3, scale 22: the LDS array 70 %
-// busy in the hash slabs), although a single lane needs ~2.  Here every lane
-// makes at most NPROBE probes; a product still without a slot is appended to
-// an LDS list (one atomic per wave) and inserted after the product loop by
-// dense waves, resuming at probe NPROBE.  A full list falls back to inline
-// probing (correct, slower).
-struct HashOvf {
-  int* count;    // LDS counter (reset by the caller before the product loop)
-  int* row;      // [cap]
-  double* val;   // [cap]
-  int cap;
-};
-__device__ __forceinline__ int lane_rank(unsigned long long m) {  // active lanes of m below this lane
+// rank of this lane among the active lanes of mask m below it
+__device__ __forceinline__ int lane_rank(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
-template <int SR, int T, int NPROBE>
-__device__ __forceinline__ void hash_acc_bounded(int* keys, double* vals, int row, double v, const HashOvf& o) {
-  unsigned h = hash_slot_t<T>(row);
-  bool done = false;
-#pragma unroll
-  for (int k = 0; k < NPROBE; ++k) {
-    if (!done) {
-      const int old = atomicCAS(&keys[h], EMPTY_KEY, row);
-      if (old == EMPTY_KEY || old == row) {
-        Sem<SR>::lds_acc(&vals[h], v);
-        done = true;
-      } else {
-        h = h + 1 == T ? 0u : h + 1;
-      }
-    }
-  }
-  const unsigned long long m = __ballot(!done);
-  if (m) {  // uniform over the wave's active lanes
-    const int leader = __ffsll((long long)m) - 1;
-    int base = 0;
-    if (lane_id() == leader) base = atomicAdd(o.count, __popcll(m));
-    base = __builtin_amdgcn_readlane(base, leader);
-    if (!done) {
-      const int idx = base + lane_rank(m);
-      if (idx < o.cap) {
-        o.row[idx] = row;
-        o.val[idx] = v;
-      } else {
-        hash_acc_from<SR, T>(keys, vals, row, v, h);
-      }
-    }
-  }
-}
-// the overflow list's items, inserted by the whole block (call after a barrier)
-template <int SR, int T, int NPROBE, int BS>
-__device__ __forceinline__ void hash_ovf_drain(int* keys, double* vals, const HashOvf& o, int n) {
-  for (int i = threadIdx.x; i < n; i += BS) {
-    const int row = o.row[i];
-    unsigned h = hash_slot_t<T>(row) + NPROBE;
-    while (h >= (unsigned)T) h -= T;
-    hash_acc_from<SR, T>(keys, vals, row, o.val[i], h);
-  }
 }
 
 // ----------------------------------------------------------------------------
@@ -601,6 +532,7 @@ constexpr int BIG_BS = CBG_BIG_BS;
 #endif
 constexpr int SPARSE_SLAB_MAX = CBG_SPARSE_SLAB_MAX;  // products of a (column, panel) pair counted by hash -> hash slab
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
+constexpr int SLAB_CNT_MASK = SLAB_SPARSE - 1;
 
 // Panel column maps of A: cmapP[r * (n+1) + k] = (first, end) of column k's
 // entries in row panel r.  A panel without rows of A(:,k) gets (q, q) with q
@@ -727,7 +659,17 @@ struct SymPanelLds {
 constexpr int SYM_OVF_CAP = CBG_SYM_OVF > 0 ? 896 : 0;
 
 // hash_claim with at most NPROBE probes; a row without a slot by then goes to
-// the overflow list (see hash_acc_bounded).  Returns 1 if this call inserted the row.
+// an LDS overflow list (one atomic per wave) that dense waves insert after the
+// product loop, resuming at probe NPROBE.  A wave's linear-probe loop runs
+// until its slowest lane has found a slot; bounding it and finishing the few
+// long probes with full waves was +1.2 % at scale 22 in the symbolic (s8 vs
+// s8n, profiles/r04_ab_hash_sym.json).  The same in the numeric hash slabs was
+// -1 % (their LDS time is not in the probes: the atomics counted by rocprofv3
+// dropped 8 %) and an expand-sort-compress numeric without a hash table
+// (products into LDS at their index, counting sort by row bucket, heads
+// compressed per bucket) -12 %: its products ran 20 % faster, the sort and
+// compression twice as long as the hash emit (profiles/r04_hash_pmc.txt).
+// Returns 1 if this call inserted the row.  A full list falls back to inline probing.
 template <int NPROBE>
 __device__ __forceinline__ int hash_claim_bounded(int* keys, unsigned h, unsigned mask, int row, int* ocount,
                                                   int* orow, int cap) {
@@ -1101,7 +1043,9 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
 // flight gather A's segments of the same panels, which then stay in L2 /
 // Infinity Cache
 #ifndef CBG_SYM_WPE  // waves per SIMD k_sym_panel is compiled for (0: the compiler's choice)
-#define CBG_SYM_WPE 0
+// 8: at most 64 VGPRs, so 4 blocks of 512 threads per CU (the LDS allows 4; at
+// 65 VGPRs only 3 fit): +4.2 % at scale 22 (profiles/r04_ab_hash_sym.json)
+#define CBG_SYM_WPE 8
 #endif
 #if CBG_SYM_WPE > 0
 #define CBG_SYM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CBG_SYM_WPE)))
@@ -1218,7 +1162,7 @@ __constant__ int c_hash_t[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
 constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS;
 __device__ __forceinline__ int slab_class(int w, int small_cap) {
   if (w & SLAB_SPARSE) {
-    const int c = w & (SLAB_SPARSE - 1);
+    const int c = w & SLAB_CNT_MASK;
     int k = 0;
     while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
     return 2 + k;
@@ -1314,7 +1258,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
       rec.r = r;
       rec.lo = d.x;
       rec.hi = d.y;
-      rec.nout = d.w & (SLAB_SPARSE - 1);
+      rec.nout = (d.w & SLAB_SPARSE) ? (d.w & SLAB_CNT_MASK) : d.w;
       rec.slot = gbm_slot ? gbm_slot[br] : -1;
       // a pair's only slab holds every row its products reach (the plan trims
       // empty fine ranges only), so A's whole panel runs are its products
@@ -2020,20 +1964,8 @@ struct SlabHashLds {
   static constexpr bool MEMB_ALIAS = CBG_HASH_MEMB_ALIAS && 2 * MEMB * 2 <= IDLE;
   static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
                                (2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2);
-  // the product loop's overflow list (hash_acc_bounded) lives in boff | cur |
-  // members, which only the emit uses: (value, row) items of 12 B, values first
-  // (boff's offset is a multiple of 8)
-  static constexpr int OFF_BOFF = T * 8 + T * 4 + BS * 8 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4;
-  static_assert(OFF_BOFF % 8 == 0, "overflow values are 8-byte aligned");
-  static constexpr int OVF_CAP = ((2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2)) / 12;
 };
-#ifndef CBG_HASH_OVF  // probes a product makes in the product loop before it is deferred (0: unbounded probing)
-#define CBG_HASH_OVF 2
-#endif
 
-// CMLEN: cmapP entries are (start, len) -- the whole-column map of the
-// column bins -- instead of the panel maps' (first, end)
-template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
 #ifndef CBG_HASH_WPE  // waves per SIMD the hash-slab kernels are compiled for (0: the compiler's choice)
 #define CBG_HASH_WPE 0
 #endif
@@ -2042,6 +1974,9 @@ template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
 #else
 #define CBG_HASH_WPE_ATTR
 #endif
+// CMLEN: cmapP entries are (start, len) -- the whole-column map of the
+// column bins -- instead of the panel maps' (first, end)
+template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
 __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, const int2* __restrict__ cmapP,
@@ -2069,12 +2004,6 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
   int* cur = boff + NB + 4;
   unsigned short* members = L::MEMB_ALIAS ? reinterpret_cast<unsigned short*>(bv) + L::MEMB
                                           : reinterpret_cast<unsigned short*>(cur + NB);
-  constexpr int NPROBE = CBG_HASH_OVF;
-  HashOvf ovf;
-  ovf.count = tmp + NW + 3;
-  ovf.val = reinterpret_cast<double*>(boff);
-  ovf.row = reinterpret_cast<int*>(ovf.val + L::OVF_CAP);
-  ovf.cap = L::OVF_CAP;
   const int tid = threadIdx.x;
   int i = blockIdx.x;
   if (i >= n) return;
@@ -2111,10 +2040,7 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
   fetch1(rec);
   fetch2(rec);
   while (true) {
-    if (tid == 0) {
-      tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
-      tmp[NW + 3] = 0;  // overflow list
-    }
+    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
     const bool pre = staged(rec);
     unsigned long long tmark = wall_clock64();
     if (CBG_VEC_INIT) {  // 16-byte LDS stores (T is a multiple of 256; vals and keys are 16-byte aligned)
@@ -2167,19 +2093,8 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
       block_products<BS>(
           pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
           [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
-          [&](const RowVal& x) {
-            if (NPROBE > 0) hash_acc_bounded<SR, T, NPROBE>(keys, vals, x.row, x.v, ovf);
-            else hash_acc_t<SR, T>(keys, vals, x.row, x.v);
-          });
+          [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
-      if (NPROBE > 0) {
-        const int no = *ovf.count;  // uniform
-        if (no > 0) {
-          hash_ovf_drain<SR, T, NPROBE, BS>(keys, vals, ovf, min(no, ovf.cap));
-          __syncthreads();
-          if (tid == 0) *ovf.count = 0;
-        }
-      }
       phase_mark(tmark, 14);
     }
     if (has_next) fetch2(nrec);
@@ -2509,6 +2424,7 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_hash<SR, 4096, CBG_HBS_4096>(at[8], ncls[8], bp, A, B, C, hs(6), df);
   launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, hs(7), df);
   launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, hs(8), df);
+
 }
 
 // (column, panel) pairs with fewer products re-mark their bitmap in the numeric

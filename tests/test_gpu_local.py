@@ -707,6 +707,32 @@ def test_phased_spgemm_matches_reference(cbg, phases):
     g.destroy()
 
 
+def test_staged_phases_regular_matrix(cbg):
+    """STAGED MemEfficientSpGEMM on a regular matrix whose two column halves (the
+    DoubleBuff stages' A slices) have identical sizes but different entries: every
+    stage of every phase frees its slices and the pool hands the same blocks out again,
+    so a column-map cache keyed on pointers and sizes would reuse the maps of another A
+    slice.  Each phase's product must equal the oracle's."""
+    rng = np.random.default_rng(7)
+    n = 4096
+    cols = np.repeat(np.arange(n), 4)
+    rows = (cols + np.tile(np.array([0, 1, 17, 301]), n) + (cols >= n // 2) * 5) % n
+    o = np.lexsort((rows, cols))
+    r, c = rows[o], cols[o]
+    Ah = dict(m=n, n=n, cp=np.arange(0, 4 * n + 1, 4, dtype=np.int64), jc=np.arange(n, dtype=np.int32),
+              ir=r.astype(np.int32), val=rng.uniform(-1, 1, 4 * n))
+    g = _self_grid(cbg)
+    A = cbg.SpParMat(cbg.Tile.from_dict(Ah), g, n, n)
+    B = cbg.SpParMat(cbg.Tile.from_dict(Ah), g, n, n)
+    ref = oracle_local(Ah, Ah)
+    bound = oracle_local(abs_tile(Ah), abs_tile(Ah))["val"]
+    for ex in (cbg.EXEC_STAGED, cbg.EXEC_PANEL):
+        C = cbg.MemEfficientSpGEMM(A, B, 4, algo=cbg.DOUBLEBUFF, exec_mode=ex)
+        assert_tiles_equal(C.tile.to_host(), ref, rtol=RTOL, bound=bound)
+        C.tile.free()
+    g.destroy()
+
+
 def test_phased_spgemm_streamed(cbg):
     """on_phase streaming: phase tiles with their column offsets add up to the full digest."""
     g = _self_grid(cbg)

@@ -14,6 +14,8 @@ for n in ${@:-2 4}; do
   python3 -c "
 import json; d = json.loads(open('gpurun_out/rehearsal_n$n.json').read().strip().splitlines()[-1])
 c = d['config']
+db = c['double_buffering']
 print('N=$n', c['grid'], c['transport'], 'nnz_C', c['nnz_C'], 'phases', c['phases'], 'ms', round(d['ms_per_step'], 2),
-      'pieces', c['double_buffering']['pieces'])"
+      'pieces', db['pieces'], 'decision', db.get('decision'), 'exposed_comm_ms', db.get('exposed_comm_ms'),
+      'bytes_bcast_rank0', db.get('bytes_bcast_rank0'))"
 done
