@@ -44,7 +44,7 @@ def load_cbg():
 # (broadcast piece by piece behind the multiply); measured per rank tile on one
 # GPU: 2x1 7 % and 4x2 2-13 % faster than 1x2 / 2x4.  --grid RxC overrides.
 GRIDS = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2), 9: (3, 3), 16: (4, 4)}
-ROUND = "r03"
+ROUND = "r04"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -104,7 +104,7 @@ def pmc_traffic(scale, ef, phases):
     committed PMC passes (profiles/<round>_traffic_s<scale>.json, made by
     tools/profile_round.sh + tools/traffic.py: FETCH_SIZE calibrated on k_digest,
     + WRITE_SIZE), this round's file first, or None."""
-    for rnd in (ROUND, "r02", "r01"):
+    for rnd in (ROUND, "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (rnd, scale))
         if not os.path.exists(path):
             continue
@@ -164,7 +164,7 @@ def cpu_baseline_reference(scale, ef, threads, algos=("synch",)):
 def cpu_baseline_s22():
     """The one-off reference run at the metric's own scale (profiles/<round>_cpu_reference_s22.json,
     tools/cpu_reference_s22.sh on the GPU box: Mult_AnXBn_Synch per B-column phase)."""
-    for rnd in (ROUND, "r02", "r01"):
+    for rnd in (ROUND, "r03", "r02", "r01"):
         path = os.path.join(REPO, "profiles", "%s_cpu_reference_s22.json" % rnd)
         if os.path.exists(path):
             with open(path) as f:
@@ -400,8 +400,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "peak_measured": peak_measured, "frac_measured": achieved / peak_measured,
                          "peak_measured_method": "16-B/lane device copy of 4 GiB x10 (read+write bytes), "
-                                                 "cbg_hbm_copy_bandwidth, best of 2 before and 2 after the "
-                                                 "timed region",
+                                                 "cbg_hbm_copy_bandwidth: the fastest of 8 copy shapes (grid-stride "
+                                                 "or one launch streaming the buffer, 1/4/8 loads in flight per "
+                                                 "lane, nontemporal or not) swept on the first call; best of 2 "
+                                                 "before and 2 after the timed region",
                          "peak_measured_runs": peaks,
                          "traffic_source": traffic_src,
                          "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",

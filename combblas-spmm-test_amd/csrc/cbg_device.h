@@ -11,9 +11,6 @@ constexpr int WAVE = 64;
 #ifndef CBG_PRODUCTS_U
 #define CBG_PRODUCTS_U 4  // products in flight per lane in wave_products (2 or 4; 8 measured equal to 4)
 #endif
-#ifndef CBG_CURSOR  // segment cursor of wave_products3: 0 bound then data, 1 together, 2 next segment prefetched
-#define CBG_CURSOR 0
-#endif
 constexpr int EMPTY_KEY = 0x7FFFFFFF;  // empty hash slot; sorts after every row id
 
 // streaming stores/loads for data written or read once (C's entries, the kept
@@ -211,46 +208,15 @@ __device__ __forceinline__ void wave_products3(const int* pref, int nseg, int u0
   if (u >= u1) return;
   int nxt = pref[sg + 1];
   auto cur = seg(sg);
-#if CBG_CURSOR == 2
-  // the next segment's bound and data are loaded when the cursor enters a
-  // segment, so a switch to the next one uses registers and only issues the
-  // following prefetch (a switch past it takes the slow path)
-  int nn = pref[sg + 2];
-  auto ncur = seg(sg + 1);
-  auto advance = [&](int v) {
-    if (v >= nxt) {
-      if (v < nn) {
-        ++sg;
-        cur = ncur;
-        nxt = nn;
-      } else {
-        do nxt = pref[++sg + 1]; while (v >= nxt);
-        cur = seg(sg);
-      }
-      nn = pref[sg + 2];
-      ncur = seg(sg + 1);
-    }
-  };
-#elif CBG_CURSOR == 1
-  // a segment's data are read together with its end bound (one LDS round trip
-  // per step instead of two; a step past an empty segment reads its data in vain)
-  auto advance = [&](int v) {
-    if (v >= nxt) {
-      do {
-        ++sg;
-        nxt = pref[sg + 1];
-        cur = seg(sg);
-      } while (v >= nxt);
-    }
-  };
-#else
+  // (reading a segment's data together with its bound, or prefetching the next
+  // segment's on entering one, measured flat / -2.5 % at scale 22:
+  // profiles/r04_ab_cursor.json -- the loop is bound by A's gathers, not by this chain)
   auto advance = [&](int v) {
     if (v >= nxt) {
       do nxt = pref[++sg + 1]; while (v >= nxt);
       cur = seg(sg);
     }
   };
-#endif
 #if CBG_PRODUCTS_U >= 4
   for (; u + 3 * WAVE < u1; u += 4 * WAVE) {
     advance(u);
