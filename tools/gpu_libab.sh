@@ -1,12 +1,12 @@
 #!/bin/bash
 # Same-box A/B of libcbg builds (tools/gpu_libab.sh): bench.py (scale ${SCALE:-22}, ${STEPS:-5} steps) for every name in
 # $VARIANTS (build/variants/<name>/libcbg.so; "tree" = the in-tree build), ${ROUNDS:-2} rounds interleaved.
-# Optional: TESTS="-k expr" runs that GPU test selection on the in-tree build first.
+# Optional: TESTS_K="expr" runs that GPU test selection (pytest -k) on the in-tree build first.
 set -o pipefail
 out=gpurun_out/ab
 mkdir -p $out
-if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest tests/test_gpu_local.py -x -q --timeout 300 --timeout-method thread $TESTS \
+if [ -n "$TESTS_K" ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_local.py -x -q --timeout 300 --timeout-method thread -k "$TESTS_K" \
     > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
   tail -1 $out/tests.log
 fi
