@@ -371,6 +371,59 @@ __device__ __forceinline__ void bitonic_sort_kv(int* keys, double* vals, int tid
   }
 }
 
+// Value of lane ^ D (D a power of two below 64) on the VALU: DPP inside rows
+// (quad_perm for 1 and 2, row_half_mirror + quad reversal for 4, row_ror:8
+// for 8) and gfx950's permlane swaps across rows (16, 32).  A __shfl_xor is a
+// ds_bpermute: an LDS instruction shared by the CU's four SIMDs, which the
+// wave sorts issued ~1200 of per wave (CBG_XOR_DPP=0 restores them).
+#ifndef CBG_XOR_DPP
+#define CBG_XOR_DPP 1
+#endif
+template <int D>
+__device__ __forceinline__ int xor_lane(int v) {
+#if CBG_XOR_DPP
+  if constexpr (D == 1) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (D == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (D == 4) {
+    const int m = __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false);  // row_half_mirror: 7 - i
+    return __builtin_amdgcn_update_dpp(0, m, 0x1B, 0xf, 0xf, false);         // quad_perm [3,2,1,0]
+  } else if constexpr (D == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  } else if constexpr (D == 16) {
+    // odd rows of the first operand <-> even rows of the second: {r0 r0 r2 r2}, {r1 r1 r3 r3}
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (threadIdx.x & 16) ? (int)r[0] : (int)r[1];
+  } else {
+    static_assert(D == 32, "xor distance");
+    // upper half of the first operand <-> lower half of the second: {lo lo}, {hi hi}
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (threadIdx.x & 32) ? (int)r[0] : (int)r[1];
+  }
+#else
+  return __shfl_xor(v, D);
+#endif
+}
+template <int D>
+__device__ __forceinline__ double xor_lane(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = xor_lane<D>((int)b), hi = xor_lane<D>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// runtime distance (unrolled loops make d a constant after inlining)
+template <typename V>
+__device__ __forceinline__ V xor_lane_d(V v, int d) {
+  switch (d) {
+    case 1: return xor_lane<1>(v);
+    case 2: return xor_lane<2>(v);
+    case 4: return xor_lane<4>(v);
+    case 8: return xor_lane<8>(v);
+    case 16: return xor_lane<16>(v);
+    default: return xor_lane<32>(v);
+  }
+}
+
 // Ascending bitonic sort of one (key, val) per lane across the 64 lanes of a
 // wave, in registers (cross-lane swaps; no LDS, no barriers).  Used for the
 // 64-slot wave tables; for 2-8 slots per lane the LDS sort was as fast.
@@ -379,8 +432,8 @@ __device__ __forceinline__ void wave_bitonic_sort_kv(int& key, double& val, int 
   for (int k = 2; k <= WAVE; k <<= 1) {
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const int ok = __shfl_xor(key, j);
-      const double ov = __shfl_xor(val, j);
+      const int ok = xor_lane_d(key, j);
+      const double ov = xor_lane_d(val, j);
       const bool up = (lane & k) == 0;     // this block of k lanes sorts ascending
       const bool lower = (lane & j) == 0;  // lower lane of the pair keeps the min when ascending
       if (lower == up ? ok < key : ok > key) {

@@ -1383,8 +1383,8 @@ __device__ __forceinline__ void wave_bitonic_sort_kvn(int (&key)[NPL], double (&
 #pragma unroll
         for (int j = 0; j < NPL; ++j) {
           const int i = j * WAVE + lane;
-          const int ok = __shfl_xor(key[j], d);
-          const double ov = __shfl_xor(val[j], d);
+          const int ok = xor_lane_d(key[j], d);
+          const double ov = xor_lane_d(val[j], d);
           const bool up = (i & k) == 0;
           const bool lower = (lane & d) == 0;
           if (lower == up ? ok < key[j] : ok > key[j]) {
@@ -1395,6 +1395,48 @@ __device__ __forceinline__ void wave_bitonic_sort_kvn(int (&key)[NPL], double (&
       }
     }
   }
+}
+
+// One step of a DPP segmented scan: lanes whose source lane (CTRL, rows ROWM)
+// holds the same key add its partial; invalid sources read EMPTY_KEY.
+template <int SR, int CTRL, int ROWM>
+__device__ __forceinline__ void seg_scan_step(int key, double& val) {
+  const int ok = __builtin_amdgcn_update_dpp(EMPTY_KEY, key, CTRL, ROWM, 0xf, false);
+  const long long b = __double_as_longlong(val);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWM, 0xf, false);
+  if (ok == key) val = Sem<SR>::add(__longlong_as_double(((long long)hi << 32) | (unsigned)lo), val);
+}
+// Inclusive segmented scan (the semiring's add) over runs of equal keys of a
+// wave whose keys are sorted ascending: Hillis-Steele with row_shr 1/2/4/8
+// inside rows of 16, then row_bcast 15/31 carry runs across rows (sorted keys:
+// equal keys at a distance are equal in between, so the carried partial
+// covers exactly the run's lanes below).  Six VALU steps instead of six
+// __shfl_up pairs (ds_bpermute).
+template <int SR>
+__device__ __forceinline__ double wave_seg_scan_sorted(int key, double val) {
+#if CBG_XOR_DPP
+  seg_scan_step<SR, 0x111, 0xf>(key, val);
+  seg_scan_step<SR, 0x112, 0xf>(key, val);
+  seg_scan_step<SR, 0x114, 0xf>(key, val);
+  seg_scan_step<SR, 0x118, 0xf>(key, val);
+  seg_scan_step<SR, 0x142, 0xa>(key, val);  // row_bcast:15 -> rows 1, 3
+  seg_scan_step<SR, 0x143, 0xc>(key, val);  // row_bcast:31 -> rows 2, 3
+#else
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < WAVE; d <<= 1) {
+    const int ok = __shfl_up(key, d);
+    const double ov = __shfl_up(val, d);
+    if (lane >= d && ok == key) val = Sem<SR>::add(ov, val);
+  }
+#endif
+  return val;
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 template <int CPW, int NPL, int SR>
@@ -1484,15 +1526,10 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
   // too), then the run that continues from the previous register's top lane
 #pragma unroll
   for (int j = 0; j < NPL; ++j) {
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-      const int ok = __shfl_up(key[j], d);
-      const double ov = __shfl_up(val[j], d);
-      if (lane >= d && ok == key[j]) val[j] = Sem<SR>::add(ov, val[j]);
-    }
+    val[j] = wave_seg_scan_sorted<SR>(key[j], val[j]);
     if (j > 0) {
       const int pk = __builtin_amdgcn_readlane(key[j - 1], WAVE - 1);
-      const double pv = __shfl(val[j - 1], WAVE - 1);
+      const double pv = readlane_f64(val[j - 1], WAVE - 1);
       if (key[j] == pk) val[j] = Sem<SR>::add(pv, val[j]);
     }
   }
@@ -1502,7 +1539,11 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
   int cj[NPL];
 #pragma unroll
   for (int j = 0; j < NPL; ++j) {
+#if CBG_XOR_DPP
+    int nk = __builtin_amdgcn_update_dpp(EMPTY_KEY, key[j], 0x130, 0xf, 0xf, false);  // wave_shl:1
+#else
     int nk = __shfl_down(key[j], 1);
+#endif
     if (j + 1 < NPL) {
       const int f = __builtin_amdgcn_readlane(key[j + 1 < NPL ? j + 1 : j], 0);
       if (lane == WAVE - 1) nk = f;
