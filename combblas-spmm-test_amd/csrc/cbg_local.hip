@@ -52,10 +52,18 @@ __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
 // ----------------------------------------------------------------------------
 // small kernels
 // ----------------------------------------------------------------------------
+// cmap and clen8 (the column lengths clamped at 255, for k_flops_seg: an
+// A-sized byte array stays in each XCD's L2, where the 8-byte cmap entries of
+// a random gather went to the Infinity Cache -- GalerkinNew's S*(AT) gathers
+// 68 M of them)
 __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int32_t* __restrict__ jc,
-                         int2* __restrict__ cmap) {
+                         int2* __restrict__ cmap, unsigned char* __restrict__ clen8) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < nzc) cmap[jc[i]] = make_int2((int)cp[i], (int)(cp[i + 1] - cp[i]));
+  if (i < nzc) {
+    const int len = (int)(cp[i + 1] - cp[i]);
+    cmap[jc[i]] = make_int2((int)cp[i], len);
+    clen8[jc[i]] = (unsigned char)min(len, 255);
+  }
 }
 
 // flops of every B column: FLOP_G lanes per column (B columns are short on
@@ -129,36 +137,44 @@ __global__ __launch_bounds__(256) void k_flops_tail(const int64_t* __restrict__ 
 // part[] and one block adds them up (a single-address atomic per block
 // serialized 60 K blocks).
 constexpr int FSEG_T = 256, FSEG_PER = 8, FSEG_E = FSEG_T * FSEG_PER;
+// the column holding each k_flops_seg block's first entry, from the column
+// side: a thread per B column writes its index for the blocks whose first
+// entry it holds (one coalesced pass over cpB instead of a 4-round dependent
+// 64-ary search at the start of every block: GalerkinNew's S*(AT), 33 K
+// blocks, 0.66 ms)
+__global__ void k_flops_starts(int64_t nzcB, const int64_t* __restrict__ cpB, int64_t* __restrict__ c_lo) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= nzcB) return;
+  const int64_t b0 = (cpB[c] + FSEG_E - 1) / FSEG_E, b1 = (cpB[c + 1] + FSEG_E - 1) / FSEG_E;
+  for (int64_t b = b0; b < b1; ++b) c_lo[b] = c;
+}
 __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB, const int64_t* __restrict__ cpB,
                                                     const int32_t* __restrict__ irB, const int2* __restrict__ cmap,
+                                                    const unsigned char* __restrict__ clen8,
+                                                    const int64_t* __restrict__ c_lo_blk,
                                                     unsigned long long* __restrict__ flops,
                                                     unsigned long long* __restrict__ part) {
   __shared__ unsigned long long lsum[FSEG_E];
   __shared__ __attribute__((aligned(16))) int head[FSEG_E];  // columns starting at each entry (empty ones too)
   __shared__ int tmp[FSEG_T / WAVE + 4];
   __shared__ unsigned long long wsum[FSEG_T / WAVE];
-  __shared__ int64_t c_lo_s;
   const int tid = threadIdx.x;
   const int64_t e0 = blockIdx.x * (int64_t)FSEG_E;
   const int64_t e1 = min(e0 + (int64_t)FSEG_E, nnzB);
-  if (tid < WAVE) {
-    // the largest c with cpB[c] <= e0 (cpB[0] = 0 <= e0 < cpB[nzcB] = nnzB)
-    int64_t lo = 0, hi = nzcB;
-    while (hi - lo > 1) {
-      const int64_t step = (hi - lo + WAVE - 1) / WAVE;
-      const int64_t idx = lo + (int64_t)tid * step;
-      const bool le = idx < hi && cpB[idx] <= e0;
-      const unsigned long long m = __ballot(le);  // lane 0 (idx = lo) is always set
-      const int64_t nlo = lo + (int64_t)(63 - __clzll((long long)m)) * step;
-      hi = min(nlo + step, hi);
-      lo = nlo;
-    }
-    if (tid == 0) c_lo_s = lo;
-  }
+  // the largest c with cpB[c] <= e0 (cpB[0] = 0 <= e0 < cpB[nzcB] = nnzB)
+  const int64_t c_lo = c_lo_blk[blockIdx.x];
+  // the entries' A lengths first: their two dependent loads overlap the
+  // column-start marking below instead of following it
+  const int i0 = tid * FSEG_PER;
+  int k[FSEG_PER];
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) k[j] = e0 + i0 + j < e1 ? irB[e0 + i0 + j] : -1;
+  int len[FSEG_PER];
+#pragma unroll
+  for (int j = 0; j < FSEG_PER; ++j) len[j] = k[j] >= 0 ? clen8[k[j]] : 0;
   for (int i = tid; i < FSEG_E; i += FSEG_T) lsum[i] = 0ull;
   for (int i = tid; i < FSEG_E / 4; i += FSEG_T) reinterpret_cast<int4*>(head)[i] = make_int4(0, 0, 0, 0);
   __syncthreads();
-  const int64_t c_lo = c_lo_s;
   // starts of the block's other columns (DCSC columns are nonempty: at most E
   // of them; an empty column would count at its position like any other)
   for (int64_t c = c_lo + 1 + tid; c < nzcB; c += FSEG_T) {
@@ -167,7 +183,6 @@ __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB
     atomicAdd(&head[p - e0], 1);
   }
   __syncthreads();
-  const int i0 = tid * FSEG_PER;
   int hd[FSEG_PER];
   {
     const int4 a = *reinterpret_cast<const int4*>(head + i0), b = *reinterpret_cast<const int4*>(head + i0 + 4);
@@ -179,12 +194,9 @@ __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB
   for (int j = 0; j < FSEG_PER; ++j) hc += hd[j];
   int ncol;
   int col = block_excl_scan<FSEG_T>(hc, tmp, &ncol);  // local column of entry i0, before its own head
-  int k[FSEG_PER];
 #pragma unroll
-  for (int j = 0; j < FSEG_PER; ++j) k[j] = e0 + i0 + j < e1 ? irB[e0 + i0 + j] : -1;
-  int len[FSEG_PER];
-#pragma unroll
-  for (int j = 0; j < FSEG_PER; ++j) len[j] = k[j] >= 0 ? cmap[k[j]].y : 0;
+  for (int j = 0; j < FSEG_PER; ++j)
+    if (len[j] == 255) len[j] = cmap[k[j]].y;  // 255 or longer
   unsigned long long acc = 0, bsum = 0;
 #pragma unroll
   for (int j = 0; j < FSEG_PER; ++j) {
@@ -308,10 +320,20 @@ __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __re
   if (big_entries && threadIdx.x == 0 && lbt) atomicAdd(big_entries + 1, lbt);
 }
 
+// hist: the bins' counts (their exclusive prefix is each bin's offset in perm);
+// cursor: per-bin fill counters, zero on entry
 __global__ __launch_bounds__(256) void k_bin_scatter(int64_t n, const uint8_t* __restrict__ bin, int nb,
-                                                     int* __restrict__ cursor, int32_t* __restrict__ perm) {
-  __shared__ int lc[MAXBINS], lb[MAXBINS];
+                                                     const int* __restrict__ hist, int* __restrict__ cursor,
+                                                     int32_t* __restrict__ perm) {
+  __shared__ int lc[MAXBINS], lb[MAXBINS], loff[MAXBINS];
   if (threadIdx.x < MAXBINS) lc[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    int a = 0;
+    for (int q = 0; q < nb; ++q) {
+      loff[q] = a;
+      a += hist[q];
+    }
+  }
   __syncthreads();
   const int64_t i0 = blockIdx.x * (int64_t)(256 * BIN_ITEMS) + threadIdx.x;
   int b[BIN_ITEMS], slot[BIN_ITEMS];
@@ -323,7 +345,8 @@ __global__ __launch_bounds__(256) void k_bin_scatter(int64_t n, const uint8_t* _
 #pragma unroll
   for (int j = 0; j < BIN_ITEMS; ++j) slot[j] = b[j] >= 0 ? atomicAdd(&lc[b[j]], 1) : 0;
   __syncthreads();
-  if (threadIdx.x < nb) lb[threadIdx.x] = lc[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], lc[threadIdx.x]) : 0;
+  if (threadIdx.x < nb)
+    lb[threadIdx.x] = loff[threadIdx.x] + (lc[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], lc[threadIdx.x]) : 0);
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < BIN_ITEMS; ++j)
@@ -2256,6 +2279,9 @@ static void launch_sym_wave(const int32_t* perm, int n, const cbg_tile& B, const
 // expand-sort-compress bin b (flops <= fmax = 64 >> (b - 1)... as CPW = 64 / fmax
 // columns per wave; one column per wave when A's rows leave no room for the
 // column bits of the sort key)
+#ifndef CBG_ESC_NPL_DEFAULT
+#define CBG_ESC_NPL_DEFAULT 1
+#endif
 template <int CPW, int NPL, int SR>
 static void launch_esc1(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
                         const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
@@ -2274,6 +2300,24 @@ static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, 
   if (fmax > 4 * WAVE) return launch_esc1<1, 8, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
   if (fmax > 2 * WAVE) return launch_esc1<1, 4, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
   if (fmax > WAVE) return launch_esc1<1, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+  // CBG_ESC_NPL=2: the bins of <= 64 flops at 2 products per lane, so a wave
+  // runs twice the columns' load chains side by side
+  static const int esc_npl = getenv("CBG_ESC_NPL") ? atoi(getenv("CBG_ESC_NPL")) : CBG_ESC_NPL_DEFAULT;
+  if (esc_npl == 2 && fmax > 2) {
+    int cpw2 = 1;
+    while (cpw2 * fmax < 2 * WAVE && cpw2 < 32) cpw2 <<= 1;  // CPW * fmax <= 128
+    int logc2 = 0;
+    while ((1 << logc2) < cpw2) ++logc2;
+    if (cpw2 >= 2 && A.m < (1LL << (31 - logc2))) {
+      switch (cpw2) {
+        case 32: return launch_esc1<32, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+        case 16: return launch_esc1<16, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+        case 8: return launch_esc1<8, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+        case 4: return launch_esc1<4, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+        default: return launch_esc1<2, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
+      }
+    }
+  }
   int cpw = 1;
   while (cpw * fmax * 2 <= WAVE && cpw < 32) cpw <<= 1;  // CPW * fmax <= 64
   int logc = 0;
@@ -2500,13 +2544,33 @@ struct Binned {
 // synchronization the caller makes anyway: bin_classify launches k_classify
 // and an async copy of the histogram; after the caller's next stream sync,
 // bin_scatter turns it into offsets and launches the scatter.
+// Small device -> host readbacks go through pinned staging (a copy into
+// pageable memory is staged by the runtime and holds the host thread once per
+// copy: ~20 us each, several per multiply): slot k of the calling thread's
+// page, read after the caller's next synchronization.
+static char* host_stage(int slot) {
+  static thread_local char* p = nullptr;
+  if (!p) CBG_HIP(hipHostMalloc((void**)&p, 8 * 4096, hipHostMallocDefault));
+  return p + (size_t)slot * 4096;
+}
+enum { STAGE_BINS_SYM = 0, STAGE_BINS_NUM = 1, STAGE_SCALARS = 2, STAGE_SLABS = 3, STAGE_AF = 4 };
 struct BinPending {
   BinThr bt;
   DBuf<uint8_t> bin;
   DBuf<int> hist;
+  char* host = nullptr;  // pinned copy of hist (after the caller's sync: read())
   std::vector<int> h;
   std::vector<unsigned long long> hf;  // flops per bin
   unsigned long long big_entries[2] = {0, 0};  // B entries of the big / thin columns
+  void read() {
+    const int* hi = reinterpret_cast<const int*>(host);
+    h.assign(hi, hi + MAXBINS);
+    const unsigned long long* be = reinterpret_cast<const unsigned long long*>(hi + 2 * MAXBINS);
+    big_entries[0] = be[0];
+    big_entries[1] = be[1];
+    const unsigned long long* bf = reinterpret_cast<const unsigned long long*>(hi + 2 * MAXBINS + 4);
+    hf.assign(bf, bf + MAXBINS);
+  }
 };
 // cpB/big_bin (mode 0): also count the B entries of the bins >= big_bin into bp.big_entries
 static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
@@ -2522,15 +2586,13 @@ static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, in
   unsigned long long* bf = reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS + 4);
   hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt,
                      bp.bin.p, bp.hist.p, fused_max, cpB, big_bin, be, bf, thin_R, thin_bin);
-  bp.h.assign(MAXBINS, 0);
-  CBG_HIP(hipMemcpyAsync(bp.h.data(), bp.hist.p, sizeof(int) * MAXBINS, hipMemcpyDeviceToHost, s));
-  bp.big_entries[0] = bp.big_entries[1] = 0;
-  if (be) CBG_HIP(hipMemcpyAsync(bp.big_entries, be, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-  bp.hf.assign(MAXBINS, 0);
-  CBG_HIP(hipMemcpyAsync(bp.hf.data(), bf, sizeof(unsigned long long) * MAXBINS, hipMemcpyDeviceToHost, s));
+  // one copy of counts | offsets | big entries | flops per bin
+  bp.host = host_stage(mode == 0 ? STAGE_BINS_SYM : STAGE_BINS_NUM);
+  CBG_HIP(hipMemcpyAsync(bp.host, bp.hist.p, sizeof(int) * (4 * MAXBINS + 4), hipMemcpyDeviceToHost, s));
 }
 static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, DeferredFree& df) {
   const int nb = bp.bt.nb;
+  if (bp.h.empty()) bp.read();
   out.count.assign(nb, 0);
   out.offset.assign(nb + 1, 0);
   for (int b = 0; b < nb; ++b) {
@@ -2538,10 +2600,9 @@ static void bin_scatter(int64_t n, BinPending& bp, Binned& out, hipStream_t s, D
     out.offset[b + 1] = out.offset[b] + bp.h[b];
   }
   out.flops = bp.hf;
-  CBG_HIP(hipMemcpyAsync(bp.hist.p + MAXBINS, out.offset.data(), sizeof(int) * nb, hipMemcpyHostToDevice, s));
   out.perm.reset(n);
-  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, bp.bin.p, nb, bp.hist.p + MAXBINS,
-                     out.perm.p);
+  hipLaunchKernelGGL(k_bin_scatter, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, bp.bin.p, nb, bp.hist.p,
+                     bp.hist.p + MAXBINS, out.perm.p);
   df.take(bp.bin);  // released after the multiply's final synchronization
   df.take(bp.hist);
 }
@@ -2623,6 +2684,7 @@ struct APrep {
   uint64_t ser_ir = 0, ser_cp = 0;  // pool allocation serials of ir / cp (0: not pool memory)
   int64_t nnz = -1, nzc = -1, m = -1, n = -1;
   DBuf<int2> cmap, cmapP;  // cmapP: built by the first call that had big columns
+  DBuf<unsigned char> clen8;  // A's column lengths clamped at 255
   int plog = -1;
   DBuf<float> valf;  // A's values as f32 (af == 1)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
@@ -2661,8 +2723,8 @@ __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __res
   }
 }
 // flops[0, nz) per B column and their total in flops[nz] (B.nnz > 0)
-static void launch_flops(const cbg_tile& B, const int2* cmap, bool A_one_per_col, int64_t* flops, hipStream_t s,
-                         DeferredFree& df) {
+static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned char* clen8, bool A_one_per_col,
+                         int64_t* flops, hipStream_t s, DeferredFree& df) {
   const int64_t nz = B.nzc;
   static const bool classic = getenv("CBG_FLOPS_CLASSIC") && atoi(getenv("CBG_FLOPS_CLASSIC"));
   if (classic) {  // a lane group per column + hub tail (before round 3)
@@ -2683,12 +2745,15 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, bool A_one_per_col
   }
   const int64_t nb = (B.nnz + FSEG_E - 1) / FSEG_E;
   DBuf<unsigned long long> part(nb);
+  DBuf<int64_t> c_lo(nb);
   CBG_HIP(hipMemsetAsync(flops, 0, sizeof(int64_t) * nz, s));
-  hipLaunchKernelGGL(k_flops_seg, dim3((unsigned)nb), dim3(FSEG_T), 0, s, nz, B.nnz, B.cp, B.ir, cmap,
+  hipLaunchKernelGGL(k_flops_starts, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, B.cp, c_lo.p);
+  hipLaunchKernelGGL(k_flops_seg, dim3((unsigned)nb), dim3(FSEG_T), 0, s, nz, B.nnz, B.cp, B.ir, cmap, clen8, c_lo.p,
                      reinterpret_cast<unsigned long long*>(flops), part.p);
   hipLaunchKernelGGL(k_sum_parts, dim3(1), dim3(1024), 0, s, part.p, nb,
                      reinterpret_cast<unsigned long long*>(flops + nz));
   df.take(part);
+  df.take(c_lo);
 }
 
 static bool af32_enabled() {
@@ -2703,6 +2768,7 @@ void aprep_begin() { aprep().active = true; }
 void aprep_end() {
   APrep& a = aprep();
   a.cmap.release();
+  a.clen8.release();
   a.cmapP.release();
   a.valf.release();
   a.af = -1;
@@ -2793,6 +2859,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                      ap.nnz == A.nnz && ap.nzc == A.nzc && ap.m == A.m && ap.n == A.n;
   if (ap.active && !a_hit) {
     ap.cmap.release();
+    ap.clen8.release();
     ap.cmapP.release();
     ap.valf.release();
     ap.af = -1;
@@ -2807,16 +2874,20 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.plog = -1;
   }
   DBuf<int2> cmap_own;
+  DBuf<unsigned char> clen8_own;
   DBuf<int2>& cmap = ap.active ? ap.cmap : cmap_own;
+  DBuf<unsigned char>& clen8 = ap.active ? ap.clen8 : clen8_own;
   if (!a_hit) {
     cmap.reset(A.n + 1);
+    clen8.reset(A.n + 1);
     CBG_HIP(hipMemsetAsync(cmap.p, 0, sizeof(int2) * (A.n + 1), s));
-    hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p);
+    CBG_HIP(hipMemsetAsync(clen8.p, 0, A.n + 1, s));
+    hipLaunchKernelGGL(k_colmap, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, cmap.p, clen8.p);
   }
 
   // flops per B column
   DBuf<int64_t> flops(nz + 1);
-  launch_flops(B, cmap.p, A.nnz == A.n && A.nzc == A.n, flops.p, s, df);
+  launch_flops(B, cmap.p, clen8.p, A.nnz == A.n && A.nzc == A.n, flops.p, s, df);
   DBuf<int32_t> cnt(nz + 1);
   CBG_HIP(hipMemsetAsync(cnt.p, 0, sizeof(int32_t) * (nz + 1), s));
   // symbolic
@@ -2824,7 +2895,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const int64_t big = big_flops(A.m);
   {
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
-    CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
+    static thread_local bool dbg_set = false;  // once (a pageable copy holds the host ~20 us)
+    if (!dbg_set && dbg) CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
+    dbg_set = true;
   }
   // symbolic bins: kSymThr (clipped at `big`), then the big columns by panel
   // group size 2^GROUP_LOG_MAX .. 1 (columns with F * g / R <= GROUP_PRODUCTS
@@ -2861,12 +2934,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     thin_R = (fused && thin_on && bp.R >= 4) ? (int)(bp.R * THIN_RATIO / ratio) : 0;
     bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
+    sp.read();
     if (thin_R && (double)sp.hf[THIN_BIN] * THIN_BYTES_PER_PRODUCT > 0.25 * device_bytes_available()) {
       // the sort's temporaries (64-bit counts, cbg_sort.hip) would take more than a
       // quarter of the device memory left: classify again without thin columns
       thin_R = 0;
       bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, 0, THIN_BIN);
       CBG_HIP(hipStreamSynchronize(s));
+      sp.read();
     }
     bin_scatter(nz, sp, sb, s, df);
     big_entries = (int64_t)sp.big_entries[0];
@@ -2927,10 +3002,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, A, cnt.p, symst[11]);
     launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, A, cnt.p, symst[12]);
   }
-  if (thin_R && sb.count[THIN_BIN] > 0)
-    thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
-                 B, cmap.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
-                 (int64_t)fused_off[SYM_FUSED_LAST + 1], s, df);
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
   const int nbig = bp.nbig;
@@ -2947,7 +3018,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
     const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
     hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p);
-    CBG_HIP(hipMemcpyAsync(&af_inexact, af_flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipMemcpyAsync(host_stage(STAGE_AF), af_flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
   }
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
@@ -3021,14 +3092,22 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
     }
   }
+  // the thin columns' sort after the big columns' launches (its host
+  // synchronizations would otherwise hold them back)
+  if (thin_R && sb.count[THIN_BIN] > 0)
+    thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
+                 B, cmap.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
+                 (int64_t)fused_off[SYM_FUSED_LAST + 1], s, df);
   join(s);
   // Everything that depends only on the per-column counts is launched now and
   // read back in ONE synchronization: nnz(C) (column pointers), the number of
   // slabs, the numeric bins' histogram and the number of nonempty C columns.
   DBuf<int64_t> colptr(nz + 1);
   exclusive_scan_i32_to_i64(cnt.p, colptr.p, nz, s, &df);
-  int64_t nnzc = 0;
-  CBG_HIP(hipMemcpyAsync(&nnzc, colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  // nnz(C), slabs, nonempty C columns, flops: one pinned slot, read after sync 2
+  int64_t* scal = reinterpret_cast<int64_t*>(host_stage(STAGE_SCALARS));
+  scal[1] = 0;
+  CBG_HIP(hipMemcpyAsync(&scal[0], colptr.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   // slab lists of big columns
   DBuf<int64_t> sbase;
   DBuf<SlabRec> slist;
@@ -3036,7 +3115,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (nbig > 0) {
     sbase.reset(nbr + 1);
     exclusive_scan_i32_to_i64(bp.nslab.p, sbase.p, nbr, s, &df);
-    CBG_HIP(hipMemcpyAsync(&nslabs, sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CBG_HIP(hipMemcpyAsync(&scal[1], sbase.p + nbr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   }
   BinPending npend;
   bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[SYM_FUSED_LAST] : 0, B.cp,
@@ -3045,11 +3124,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
   exclusive_scan_i64(flag.p, pos.p, nz, s, &df);
-  int64_t nzcC = 0, flops_total = 0;
-  CBG_HIP(hipMemcpyAsync(&nzcC, pos.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  CBG_HIP(hipMemcpyAsync(&flops_total, flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&scal[2], pos.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CBG_HIP(hipMemcpyAsync(&scal[3], flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));  // host sync 2 of 4
+  const int64_t nnzc = scal[0], nzcC = scal[2], flops_total = scal[3];
+  nslabs = scal[1];
   if (sym_only) {
     df.synced = true;
     if (st) {
@@ -3064,6 +3144,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     return;
   }
   if (af_flag.p) {
+    af_inexact = *reinterpret_cast<const int*>(host_stage(STAGE_AF));
     af = af_inexact ? 0 : 1;
     if (ap.active) ap.af = af;
     if (!af) valf.release();
@@ -3098,8 +3179,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 2 * NK * sizeof(int), s, nbig, bp.R,
                        bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, counters.p + NK, slist.p, bp.perm_big, B.cp, colptr.p,
                        bp.gbm_slot.p, bp.plog, A.m);
-    CBG_HIP(hipMemcpyAsync(ncls, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
+    int* ncls_h = reinterpret_cast<int*>(host_stage(STAGE_SLABS));
+    CBG_HIP(hipMemcpyAsync(ncls_h, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));  // host sync 3 of 4: the slab classes' sizes
+    std::memcpy(ncls, ncls_h, sizeof(int) * SLAB_NCLS);
     df.take(counters);
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)

@@ -330,9 +330,13 @@ __global__ __launch_bounds__(SCAN_BS) void k_scan_tile(const TI* __restrict__ in
   if (tid == 0) tile_sum[blockIdx.x] = wsum[SCAN_BS / WAVE];
 }
 
-__global__ void k_scan_add(int64_t* __restrict__ out, int64_t n, const int64_t* __restrict__ toff) {
+// also out[n] = the total (toff[nt]): a separate 8-byte device copy is a blit
+// kernel that waits for a free CU slot behind a concurrent stream's kernels
+// (up to 150 us seen in GalerkinNew's thin-column sort)
+__global__ void k_scan_add(int64_t* __restrict__ out, int64_t n, const int64_t* __restrict__ toff, int64_t nt) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) out[i] += toff[i / SCAN_TILE];
+  if (i == 0) out[n] = toff[nt];
 }
 
 template <class TI>
@@ -349,8 +353,7 @@ static void scan_impl(const TI* in, int64_t* out, int64_t n, hipStream_t s, Defe
   DBuf<int64_t> sums(nt), offs(nt + 1);
   hipLaunchKernelGGL(k_scan_tile<TI>, dim3((unsigned)nt), dim3(SCAN_BS), 0, s, in, n, out, sums.p);
   scan_impl<int64_t>(sums.p, offs.p, nt, s, df);
-  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, n, offs.p);
-  CBG_HIP(hipMemcpyAsync(out + n, offs.p + nt, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out, n, offs.p, nt);
   if (df) {  // released when the caller's work on `s` has been synchronized
     df->take(sums);
     df->take(offs);
