@@ -23,6 +23,7 @@
 // take consecutive products, so reads of A's columns are coalesced whatever
 // their length (R-MAT hub columns included).
 #include <cstring>
+#include <type_traits>
 
 #include "cbg_device.h"
 #include "cbg_internal.h"
@@ -137,6 +138,19 @@ __global__ __launch_bounds__(256) void k_flops_tail(const int64_t* __restrict__ 
 // part[] and one block adds them up (a single-address atomic per block
 // serialized 60 K blocks).
 constexpr int FSEG_T = 256, FSEG_PER = 8, FSEG_E = FSEG_T * FSEG_PER;
+// k[j] = ir[e + j] (j < 8; -1 at or past end); two 16-byte loads when aligned:
+// a lane's 8 consecutive entries as 8 scalar loads touch 16 lines per wave
+// instruction, eight times over
+__device__ __forceinline__ void load8_rows(const int32_t* __restrict__ ir, int64_t e, int64_t end, int (&k)[8]) {
+  if (e + 8 <= end && ((reinterpret_cast<uintptr_t>(ir + e) & 15) == 0)) {
+    const int4 a = reinterpret_cast<const int4*>(ir + e)[0];
+    const int4 b = reinterpret_cast<const int4*>(ir + e)[1];
+    k[0] = a.x, k[1] = a.y, k[2] = a.z, k[3] = a.w, k[4] = b.x, k[5] = b.y, k[6] = b.z, k[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k[j] = e + j < end ? ir[e + j] : -1;
+  }
+}
 // the column holding each k_flops_seg block's first entry, from the column
 // side: a thread per B column writes its index for the blocks whose first
 // entry it holds (one coalesced pass over cpB instead of a 4-round dependent
@@ -167,8 +181,7 @@ __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB
   // column-start marking below instead of following it
   const int i0 = tid * FSEG_PER;
   int k[FSEG_PER];
-#pragma unroll
-  for (int j = 0; j < FSEG_PER; ++j) k[j] = e0 + i0 + j < e1 ? irB[e0 + i0 + j] : -1;
+  load8_rows(irB, e0 + i0, e1, k);
   int len[FSEG_PER];
 #pragma unroll
   for (int j = 0; j < FSEG_PER; ++j) len[j] = k[j] >= 0 ? clen8[k[j]] : 0;
@@ -223,6 +236,11 @@ __global__ __launch_bounds__(FSEG_T) void k_flops_seg(int64_t nzcB, int64_t nnzB
     part[blockIdx.x] = t;
   }
 }
+// (An LDS-free variant -- a wave per 512 entries, column starts from a global
+// bitmap, a DPP segmented scan of the lanes' last-column sums and one global
+// atomic per column piece -- measured slower than k_flops_seg: GalerkinNew at
+// scale 22 6.76-6.96 vs 6.62-6.80 ms, removed.)
+
 // flops when every A column has exactly one entry: the B column lengths, and
 // their total (nnz(B)) in flops[nz]
 __global__ void k_flops_unit(int64_t nz, const int64_t* __restrict__ cpB, int64_t* __restrict__ flops) {
@@ -356,6 +374,10 @@ __global__ __launch_bounds__(256) void k_bin_scatter(int64_t n, const uint8_t* _
 struct RowVal {
   int row;
   double v;
+};
+struct alignas(8) PackedRV {
+  int row;
+  float v;
 };
 
 // claim `row` in an LDS hash of mask + 1 slots (linear probing from h):
@@ -1737,11 +1759,17 @@ constexpr int SLAB_SMALL_CAP = CBG_SLAB_SMALL_CAP, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
 
 // A's (row, value) of product position q
-// (VA = float: A's values narrowed losslessly, see k_vals_f32; the widening is exact)
+// (VA = float: A's values narrowed losslessly, see k_vals_f32; the widening is
+// exact; VA = PackedRV: the same as (row, f32) records, one gather per product)
 template <int SR, typename VA>
 __device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, const VA* __restrict__ valA, int q,
                                            double b, int lo) {
-  return RowVal{irA[q] - lo, Sem<SR>::mul((double)valA[q], b)};
+  if constexpr (std::is_same<VA, PackedRV>::value) {
+    const PackedRV e = valA[q];
+    return RowVal{e.row - lo, Sem<SR>::mul((double)e.v, b)};
+  } else {
+    return RowVal{irA[q] - lo, Sem<SR>::mul((double)valA[q], b)};
+  }
 }
 
 template <int SR, int BS, typename VA>
@@ -2422,6 +2450,7 @@ struct BigPlan {
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
   const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
+  const PackedRV* valAp = nullptr;  // ... and as (row, f32) records (CBG_APACK)
 };
 
 
@@ -2442,8 +2471,9 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                        A.n + 1, A.ir, valA, C.ir, C.val);
   };
-  static int per_cu_d = 0, per_cu_f = 0;
-  if (bp.valAf) go(k_num_slab_hash<SR, T, BS, false, float>, bp.valAf, per_cu_f);
+  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
+  if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp, per_cu_p);
+  else if (bp.valAf) go(k_num_slab_hash<SR, T, BS, false, float>, bp.valAf, per_cu_f);
   else go(k_num_slab_hash<SR, T, BS, false, double>, A.val, per_cu_d);
   df.take(queue);
 }
@@ -2465,8 +2495,9 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                        A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p);
   };
-  static int per_cu_d = 0, per_cu_f = 0;
-  if (bp.valAf) go(k_num_slab<SR, CAP, BS, float>, bp.valAf, per_cu_f);
+  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
+  if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV>, bp.valAp, per_cu_p);
+  else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float>, bp.valAf, per_cu_f);
   else go(k_num_slab<SR, CAP, BS, double>, A.val, per_cu_d);
   df.take(queue);
 }
@@ -2687,6 +2718,7 @@ struct APrep {
   DBuf<unsigned char> clen8;  // A's column lengths clamped at 255
   int plog = -1;
   DBuf<float> valf;  // A's values as f32 (af == 1)
+  DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
 
@@ -2697,7 +2729,9 @@ struct APrep {
 // (stops early once some value is inexact: the copy is then not used --
 // GalerkinNew's A = L + D carries random diagonal values, and each of its
 // products checked all 68 M values for nothing: 0.21 ms)
-__global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __restrict__ f, int* __restrict__ inexact) {
+// pk (optional): A's (row, f32 value) records, one 8-byte gather per numeric product
+__global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __restrict__ f, int* __restrict__ inexact,
+                           const int32_t* __restrict__ ir, PackedRV* __restrict__ pk) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   while (i < n) {
@@ -2709,6 +2743,7 @@ __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __res
         const double x = v[i];
         const float y = (float)x;
         f[i] = y;
+        if (pk) pk[i] = PackedRV{ir[i], y};
         bad |= !((double)y == x);
       }
     }
@@ -2756,6 +2791,11 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned cha
   df.take(c_lo);
 }
 
+// CBG_APACK=0: the slab kernels read A's rows and f32 values from two arrays
+static bool apack_enabled() {
+  static const char* e = getenv("CBG_APACK");
+  return !(e && !strcmp(e, "0"));
+}
 static bool af32_enabled() {
   static const char* e = getenv("CBG_AF32");
   return !(e && !strcmp(e, "0"));
@@ -2771,6 +2811,7 @@ void aprep_end() {
   a.clen8.release();
   a.cmapP.release();
   a.valf.release();
+  a.valp.release();
   a.af = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
@@ -2862,6 +2903,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.clen8.release();
     ap.cmapP.release();
     ap.valf.release();
+    ap.valp.release();
     ap.af = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
@@ -3010,14 +3052,18 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // verdict is read back with host sync 2)
   DBuf<float> valf_own;
   DBuf<float>& valf = ap.active ? ap.valf : valf_own;
+  DBuf<PackedRV> valp_own;
+  DBuf<PackedRV>& valp = ap.active ? ap.valp : valp_own;
   int af = ap.active ? ap.af : -1, af_inexact = 0;
   DBuf<int> af_flag;
   if (nbig > 0 && af < 0 && af32_enabled() && !sym_only) {
     valf.reset(A.nnz);
+    if (apack_enabled()) valp.reset(A.nnz);
     af_flag.reset(1);
     CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
     const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
-    hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p);
+    hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p, A.ir,
+                       valp.p);
     CBG_HIP(hipMemcpyAsync(host_stage(STAGE_AF), af_flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
   }
   if (nbig > 0) {
@@ -3147,9 +3193,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     af_inexact = *reinterpret_cast<const int*>(host_stage(STAGE_AF));
     af = af_inexact ? 0 : 1;
     if (ap.active) ap.af = af;
-    if (!af) valf.release();
+    if (!af) {
+      valf.release();
+      valp.release();
+    }
   }
   if (af == 1) bp.valAf = valf.p;
+  if (af == 1 && valp.p) bp.valAp = valp.p;
   {
     // test hook (CBG_FAULT_C_BYTES, read per call): C larger than this fails as
     // an out-of-memory would, after the symbolic pass -- the phase splitting of
