@@ -214,9 +214,10 @@ void exclusive_scan_i32_to_i64(const int32_t* in, int64_t* out, int64_t n, hipSt
 // (fthin products in all) expanded, sorted and reduced into tir/tval[base ...];
 // cnt[col] = their nnz, tslot[col] = their first temporary position
 // (E = their B entries); thin_copy moves them to C after the column scan
+// (ainl: optional inline records of A's columns, see k_inline_cols)
 void thin_columns(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-                  const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval,
-                  int64_t base, hipStream_t s, DeferredFree& df);
+                  const int2* cmap, const int4* ainl, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir,
+                  double* tval, int64_t base, hipStream_t s, DeferredFree& df);
 void thin_copy(const int32_t* perm, int n, const int64_t* tslot, const int32_t* cnt, const int64_t* colptr,
                const int32_t* tir, const double* tval, int32_t* out_ir, double* out_val, hipStream_t s);
 

@@ -67,6 +67,23 @@ __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int3
   }
 }
 
+// A's columns as inline records for the small-column passes (INL): x = length,
+// y = the row of a one-entry column, else its start, zw = that entry's value
+__global__ void k_inline_cols(int64_t n1, const int2* __restrict__ cmap, const int32_t* __restrict__ irA,
+                              const double* __restrict__ valA, int4* __restrict__ ainl) {
+  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (k >= n1) return;
+  const int2 m = cmap[k];
+  int4 r = make_int4(m.y, m.x, 0, 0);
+  if (m.y == 1) {
+    const long long b = __double_as_longlong(valA[m.x]);
+    r.y = irA[m.x];
+    r.z = (int)b;
+    r.w = (int)(b >> 32);
+  }
+  ainl[k] = r;
+}
+
 // flops of every B column: FLOP_G lanes per column (B columns are short on
 // average; a whole wave per column would leave most lanes idle).  A group
 // sums at most FLOP_HEAD entries of its column and queues a longer column
@@ -1484,10 +1501,15 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-template <int CPW, int NPL, int SR>
+// INL: A's columns as inline records (k_inline_cols): {len, row of the only
+// entry or the start, the only entry's value}; a product of a one-entry A
+// column takes its row and value from the B entry's lane (shuffles) instead of
+// two random gathers -- GalerkinNew's S = T^T, Poisson(1) entries per column
+template <int CPW, int NPL, int SR, bool INL>
 __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ perm, int n, int fmax,
                                                   const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
                                                   const double* __restrict__ valB, const int2* __restrict__ cmap,
+                                                  const int4* __restrict__ ainl,
                                                   const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ tir,
                                                   double* __restrict__ tval, int64_t slot_base,
@@ -1526,12 +1548,19 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
     const int ex_c = __shfl(bexc, c);
     const int64_t p0_c = __shfl(p0, c);
     int s = 0, len = 0;
-    double bv = 0.0;
+    double bv = 0.0, v0 = 0.0;
     if (e < totalB) {
       const int64_t p = p0_c + (e - ex_c);
-      const int2 m = cmap[irB[p]];
-      s = m.x;
-      len = m.y;
+      if constexpr (INL) {
+        const int4 r = ainl[irB[p]];
+        len = r.x;
+        s = r.y;
+        v0 = __hiloint2double(r.w, r.z);
+      } else {
+        const int2 m = cmap[irB[p]];
+        s = m.x;
+        len = m.y;
+      }
       bv = valB[p];
     }
     const int pincl = wave_incl_scan(len);
@@ -1553,10 +1582,21 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
       const int o = lo;
       const int o_s = __shfl(s, o), o_ex = __shfl(pincl - len, o), o_c = __shfl(c, o);
       const double o_bv = __shfl(bv, o);
+      bool one = false;
+      double o_v0 = 0.0;
+      if constexpr (INL) {
+        one = __shfl(len, o) == 1;
+        o_v0 = __shfl(v0, o);
+      }
       if (q >= 0 && q < ptot) {
-        const int a = o_s + (q - o_ex);
-        key[j] = (o_c << SH) | irA[a];
-        val[j] = Sem<SR>::mul(valA[a], o_bv);
+        if (INL && one) {
+          key[j] = (o_c << SH) | o_s;
+          val[j] = Sem<SR>::mul(o_v0, o_bv);
+        } else {
+          const int a = o_s + (q - o_ex);
+          key[j] = (o_c << SH) | irA[a];
+          val[j] = Sem<SR>::mul(valA[a], o_bv);
+        }
       }
     }
     pbase += ptot;
@@ -2307,58 +2347,46 @@ static void launch_sym_wave(const int32_t* perm, int n, const cbg_tile& B, const
 // expand-sort-compress bin b (flops <= fmax = 64 >> (b - 1)... as CPW = 64 / fmax
 // columns per wave; one column per wave when A's rows leave no room for the
 // column bits of the sort key)
-#ifndef CBG_ESC_NPL_DEFAULT
-#define CBG_ESC_NPL_DEFAULT 1
-#endif
+// (2 products per lane for the bins of <= 64 flops, twice the columns per
+// wave: GalerkinNew 7.33 vs 7.26 ms, not kept)
 template <int CPW, int NPL, int SR>
 static void launch_esc1(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
-                        const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
-                        hipStream_t s) {
-  hipLaunchKernelGGL((k_esc_wave<CPW, NPL, SR>), dim3(nblk((n + CPW - 1) / CPW, 4)), dim3(256), 0, s, perm, n, fmax,
-                     B.cp, B.ir, B.val, cmap, A.ir, A.val, cnt, tir + base, tval + base, base, tslot);
+                        const int4* ainl, const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base,
+                        int64_t* tslot, hipStream_t s) {
+  const dim3 g(nblk((n + CPW - 1) / CPW, 4));
+  if (ainl)
+    hipLaunchKernelGGL((k_esc_wave<CPW, NPL, SR, true>), g, dim3(256), 0, s, perm, n, fmax, B.cp, B.ir, B.val, cmap,
+                       ainl, A.ir, A.val, cnt, tir + base, tval + base, base, tslot);
+  else
+    hipLaunchKernelGGL((k_esc_wave<CPW, NPL, SR, false>), g, dim3(256), 0, s, perm, n, fmax, B.cp, B.ir, B.val, cmap,
+                       ainl, A.ir, A.val, cnt, tir + base, tval + base, base, tslot);
 }
 // expand-sort-compress bin of flops <= fmax: CPW = 64 * NPL / fmax columns per
 // wave (one column per wave when A's rows leave no room for the column bits of
 // the sort key); fmax 128 / 256 / 512 sort 2 / 4 / 8 products per lane
 template <int SR>
-static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
+static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap, const int4* ainl,
                        const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base, int64_t* tslot,
                        hipStream_t s) {
   if (n <= 0) return;
-  if (fmax > 4 * WAVE) return launch_esc1<1, 8, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-  if (fmax > 2 * WAVE) return launch_esc1<1, 4, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-  if (fmax > WAVE) return launch_esc1<1, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-  // CBG_ESC_NPL=2: the bins of <= 64 flops at 2 products per lane, so a wave
-  // runs twice the columns' load chains side by side
-  static const int esc_npl = getenv("CBG_ESC_NPL") ? atoi(getenv("CBG_ESC_NPL")) : CBG_ESC_NPL_DEFAULT;
-  if (esc_npl == 2 && fmax > 2) {
-    int cpw2 = 1;
-    while (cpw2 * fmax < 2 * WAVE && cpw2 < 32) cpw2 <<= 1;  // CPW * fmax <= 128
-    int logc2 = 0;
-    while ((1 << logc2) < cpw2) ++logc2;
-    if (cpw2 >= 2 && A.m < (1LL << (31 - logc2))) {
-      switch (cpw2) {
-        case 32: return launch_esc1<32, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-        case 16: return launch_esc1<16, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-        case 8: return launch_esc1<8, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-        case 4: return launch_esc1<4, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-        default: return launch_esc1<2, 2, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s);
-      }
-    }
-  }
+#define CBG_ESC_ARGS perm, n, fmax, B, cmap, ainl, A, cnt, tir, tval, base, tslot, s
+  if (fmax > 4 * WAVE) return launch_esc1<1, 8, SR>(CBG_ESC_ARGS);
+  if (fmax > 2 * WAVE) return launch_esc1<1, 4, SR>(CBG_ESC_ARGS);
+  if (fmax > WAVE) return launch_esc1<1, 2, SR>(CBG_ESC_ARGS);
   int cpw = 1;
   while (cpw * fmax * 2 <= WAVE && cpw < 32) cpw <<= 1;  // CPW * fmax <= 64
   int logc = 0;
   while ((1 << logc) < cpw) ++logc;
   if (A.m >= (1LL << (31 - logc))) cpw = 1;  // key = c << (31 - logc) | row must stay below EMPTY_KEY
   switch (cpw) {
-    case 32: launch_esc1<32, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
-    case 16: launch_esc1<16, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
-    case 8: launch_esc1<8, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
-    case 4: launch_esc1<4, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
-    case 2: launch_esc1<2, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
-    default: launch_esc1<1, 1, SR>(perm, n, fmax, B, cmap, A, cnt, tir, tval, base, tslot, s); break;
+    case 32: launch_esc1<32, 1, SR>(CBG_ESC_ARGS); break;
+    case 16: launch_esc1<16, 1, SR>(CBG_ESC_ARGS); break;
+    case 8: launch_esc1<8, 1, SR>(CBG_ESC_ARGS); break;
+    case 4: launch_esc1<4, 1, SR>(CBG_ESC_ARGS); break;
+    case 2: launch_esc1<2, 1, SR>(CBG_ESC_ARGS); break;
+    default: launch_esc1<1, 1, SR>(CBG_ESC_ARGS); break;
   }
+#undef CBG_ESC_ARGS
 }
 template <int LOGT, int BS>
 static void launch_sym_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
@@ -3002,6 +3030,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     fused_slot.reset(nz);
     CBG_HIP(hipMemsetAsync(fused_slot.p, 0xff, sizeof(int64_t) * nz, s));  // -1: not fused (before the fork)
   }
+  // inline records of A's columns for the small-column and thin passes when A's
+  // columns are short (<= 2 entries on average) and each entry is gathered many
+  // times (flops >= 4 nnz(A)): GalerkinNew's S*(AT), S = T^T (CBG_AINL=0: off)
+  DBuf<int4> ainl;
+  {
+    static const bool ainl_on = !(getenv("CBG_AINL") && !strcmp(getenv("CBG_AINL"), "0"));
+    unsigned long long fsmall = 0;
+    for (int b = 1; b < NSMALL; ++b) fsmall += sb.flops[b];
+    fsmall += thin_R ? sb.flops[THIN_BIN] : 0;
+    if (ainl_on && fused && A.nnz <= 2 * A.nzc && (double)fsmall >= 4.0 * (double)A.nnz) {
+      ainl.reset(A.n + 1);
+      hipLaunchKernelGGL(k_inline_cols, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, A.ir, A.val,
+                         ainl.p);
+    }
+  }
   fork(s);
   // streams of the small symbolic bins (balance_bins; the fused bins also do
   // their numeric work: cost 2 per flop)
@@ -3027,10 +3070,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       fused_val.reset(ftot + 1);
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) {
         if (semiring == CBG_MIN_PLUS)
-          launch_esc<1>(at(b), sb.count[b], fmax_of(b), B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p,
+          launch_esc<1>(at(b), sb.count[b], fmax_of(b), B, cmap.p, ainl.p, A, cnt.p, fused_ir.p, fused_val.p,
                         (int64_t)fused_off[b], fused_slot.p, symst[b]);
         else
-          launch_esc<0>(at(b), sb.count[b], fmax_of(b), B, cmap.p, A, cnt.p, fused_ir.p, fused_val.p,
+          launch_esc<0>(at(b), sb.count[b], fmax_of(b), B, cmap.p, ainl.p, A, cnt.p, fused_ir.p, fused_val.p,
                         (int64_t)fused_off[b], fused_slot.p, symst[b]);
       }
     } else {
@@ -3142,7 +3185,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // synchronizations would otherwise hold them back)
   if (thin_R && sb.count[THIN_BIN] > 0)
     thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
-                 B, cmap.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
+                 B, cmap.p, ainl.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
                  (int64_t)fused_off[SYM_FUSED_LAST + 1], s, df);
   join(s);
   // Everything that depends only on the per-column counts is launched now and

@@ -34,8 +34,8 @@ __global__ void k_thin_sizes(const int32_t* __restrict__ perm, int n, const int6
 // flattened thin entry e (of E): its column index, B position and product count
 __global__ void k_thin_entries(const int32_t* __restrict__ perm, int n, const int64_t* __restrict__ eoff,
                                int64_t E, const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                               const int2* __restrict__ cmap, int32_t* __restrict__ ecol, int64_t* __restrict__ epos,
-                               int64_t* __restrict__ elen) {
+                               const int2* __restrict__ cmap, const int4* __restrict__ ainl,
+                               int32_t* __restrict__ ecol, int64_t* __restrict__ epos, int64_t* __restrict__ elen) {
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e >= E) return;
   int lo = 0, hi = n - 1;  // the last i with eoff[i] <= e
@@ -46,16 +46,18 @@ __global__ void k_thin_entries(const int32_t* __restrict__ perm, int n, const in
   const int64_t p = cpB[perm[lo]] + (e - eoff[lo]);
   ecol[e] = lo;
   epos[e] = p;
-  elen[e] = cmap[irB[p]].y;
+  elen[e] = ainl ? ainl[irB[p]].x : cmap[irB[p]].y;
 }
 
 // a wave per 64 flattened entries: their products, one per lane per round,
 // from the wave's first output position poff[e0]
-template <typename K, int SR>
+// INL: a one-entry A column's row and value come from the entry's lane (k_inline_cols)
+template <typename K, int SR, bool INL>
 __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* __restrict__ ecol,
                                                      const int64_t* __restrict__ epos,
                                                      const int64_t* __restrict__ poff, const int32_t* __restrict__ irB,
                                                      const double* __restrict__ valB, const int2* __restrict__ cmap,
+                                                     const int4* __restrict__ ainl,
                                                      const int32_t* __restrict__ irA, const double* __restrict__ valA,
                                                      int rowbits, K* __restrict__ keys, double* __restrict__ vals) {
   const int64_t e0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE * WAVE;
@@ -63,12 +65,19 @@ __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* _
   const int lane = lane_id();
   const int64_t e = e0 + lane;
   int s = 0, len = 0, c = 0;
-  double bv = 0.0;
+  double bv = 0.0, v0 = 0.0;
   if (e < E) {
     const int64_t p = epos[e];
-    const int2 m = cmap[irB[p]];
-    s = m.x;
-    len = m.y;
+    if constexpr (INL) {
+      const int4 r = ainl[irB[p]];
+      len = r.x;
+      s = r.y;
+      v0 = __hiloint2double(r.w, r.z);
+    } else {
+      const int2 m = cmap[irB[p]];
+      s = m.x;
+      len = m.y;
+    }
     bv = valB[p];
     c = ecol[e];
   }
@@ -86,10 +95,21 @@ __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* _
     }
     const int e_s = __shfl(s, lo), e_ex = __shfl(incl - len, lo), e_c = __shfl(c, lo);
     const double e_bv = __shfl(bv, lo);
+    bool one = false;
+    double e_v0 = 0.0;
+    if constexpr (INL) {
+      one = __shfl(len, lo) == 1;
+      e_v0 = __shfl(v0, lo);
+    }
     if (q < total) {
-      const int a = e_s + (q - e_ex);
-      keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)irA[a];
-      vals[o + q] = Sem<SR>::mul(valA[a], e_bv);
+      if (INL && one) {
+        keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)e_s;
+        vals[o + q] = Sem<SR>::mul(e_v0, e_bv);
+      } else {
+        const int a = e_s + (q - e_ex);
+        keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)irA[a];
+        vals[o + q] = Sem<SR>::mul(valA[a], e_bv);
+      }
     }
   }
 }
@@ -117,24 +137,30 @@ __global__ void k_thin_slots(const int32_t* __restrict__ perm, int n, const int6
 
 template <typename K>
 void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-               const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base,
-               int rowbits, int colbits, hipStream_t s, DeferredFree& df) {
+               const int2* cmap, const int4* ainl, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir,
+               double* tval, int64_t base, int rowbits, int colbits, hipStream_t s, DeferredFree& df) {
   DBuf<int64_t> nbe(n + 1), eoff(n + 1), first(n);
   hipLaunchKernelGGL(k_thin_sizes, dim3((n + 255) / 256), dim3(256), 0, s, perm, n, B.cp, nbe.p);
   exclusive_scan_i64(nbe.p, eoff.p, n, s, &df);
   DBuf<int32_t> ecol(E);
   DBuf<int64_t> epos(E), elen(E + 1), poff(E + 1);
   hipLaunchKernelGGL(k_thin_entries, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, perm, n, eoff.p, E, B.cp,
-                     B.ir, cmap, ecol.p, epos.p, elen.p);
+                     B.ir, cmap, ainl, ecol.p, epos.p, elen.p);
   exclusive_scan_i64(elen.p, poff.p, E, s, &df);
   DBuf<K> k0(fthin), uk(fthin);
   DBuf<double> v0(fthin);
-  if (semiring == CBG_MIN_PLUS)
-    hipLaunchKernelGGL((k_thin_expand<K, 1>), dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, ecol.p, epos.p,
-                       poff.p, B.ir, B.val, cmap, A.ir, A.val, rowbits, k0.p, v0.p);
-  else
-    hipLaunchKernelGGL((k_thin_expand<K, 0>), dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, ecol.p, epos.p,
-                       poff.p, B.ir, B.val, cmap, A.ir, A.val, rowbits, k0.p, v0.p);
+  const dim3 g((unsigned)((E + 255) / 256));
+#define CBG_THIN_EXPAND(SR, INL)                                                                                  \
+  hipLaunchKernelGGL((k_thin_expand<K, SR, INL>), g, dim3(256), 0, s, E, ecol.p, epos.p, poff.p, B.ir, B.val, cmap, \
+                     ainl, A.ir, A.val, rowbits, k0.p, v0.p)
+  if (semiring == CBG_MIN_PLUS) {
+    if (ainl) CBG_THIN_EXPAND(1, true);
+    else CBG_THIN_EXPAND(1, false);
+  } else {
+    if (ainl) CBG_THIN_EXPAND(0, true);
+    else CBG_THIN_EXPAND(0, false);
+  }
+#undef CBG_THIN_EXPAND
   const int end_bit = rowbits + colbits;
   radix_sort_pairs<K>(k0, v0, fthin, end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1, s);
   const int64_t nruns = reduce_by_key<K>(k0.p, v0.p, fthin, semiring, uk.p, tval + base, s);
@@ -155,26 +181,27 @@ void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_t
 }
 
 void thin_any(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-              const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval, int64_t base,
-              hipStream_t s, DeferredFree& df) {
+              const int2* cmap, const int4* ainl, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir,
+              double* tval, int64_t base, hipStream_t s, DeferredFree& df) {
   int rowbits = 1, colbits = 1;
   while ((1LL << rowbits) < A.m) ++rowbits;
   while ((1LL << colbits) < (int64_t)n) ++colbits;
   // (column, row) keys in 32 bits when they fit: fewer radix passes, half the key traffic
   if (rowbits + colbits <= 32)
-    thin_impl<uint32_t>(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, rowbits, colbits, s, df);
+    thin_impl<uint32_t>(perm, n, E, fthin, A, B, cmap, ainl, semiring, cnt, tslot, tir, tval, base, rowbits, colbits, s,
+                        df);
   else
-    thin_impl<unsigned long long>(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, rowbits,
+    thin_impl<unsigned long long>(perm, n, E, fthin, A, B, cmap, ainl, semiring, cnt, tslot, tir, tval, base, rowbits,
                                   colbits, s, df);
 }
 
 }  // namespace
 
 void thin_columns(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_tile& A, const cbg_tile& B,
-                  const int2* cmap, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir, double* tval,
-                  int64_t base, hipStream_t s, DeferredFree& df) {
+                  const int2* cmap, const int4* ainl, int semiring, int32_t* cnt, int64_t* tslot, int32_t* tir,
+                  double* tval, int64_t base, hipStream_t s, DeferredFree& df) {
   if (n <= 0 || fthin <= 0 || E <= 0) return;
-  thin_any(perm, n, E, fthin, A, B, cmap, semiring, cnt, tslot, tir, tval, base, s, df);
+  thin_any(perm, n, E, fthin, A, B, cmap, ainl, semiring, cnt, tslot, tir, tval, base, s, df);
 }
 
 // the thin columns' entries -> C: a block per column (k_copy_fused's few
