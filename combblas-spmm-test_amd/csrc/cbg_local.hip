@@ -2348,7 +2348,9 @@ static void launch_sym_wave(const int32_t* perm, int n, const cbg_tile& B, const
 // columns per wave; one column per wave when A's rows leave no room for the
 // column bits of the sort key)
 // (2 products per lane for the bins of <= 64 flops, twice the columns per
-// wave: GalerkinNew 7.33 vs 7.26 ms, not kept)
+// wave: GalerkinNew 7.33 vs 7.26 ms; 16 per lane for the 513-1024-flop bin
+// instead of its block hash passes: 148 VGPRs, 3 waves per SIMD, 8.47 vs
+// 6.28 ms and 463 vs 447 ms at scale 22 -- neither kept)
 template <int CPW, int NPL, int SR>
 static void launch_esc1(const int32_t* perm, int n, int fmax, const cbg_tile& B, const int2* cmap,
                         const int4* ainl, const cbg_tile& A, int32_t* cnt, int32_t* tir, double* tval, int64_t base,
@@ -3183,6 +3185,22 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   // the thin columns' sort after the big columns' launches (its host
   // synchronizations would otherwise hold them back)
+  {
+    // CBG_DBG bit 16: the symbolic bins' sizes
+    static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
+    if (dbg & 16) {
+      unsigned long long fs = 0, fh = 0, fb = 0;
+      for (int b = 1; b <= SYM_FUSED_LAST; ++b) fs += sb.flops[b];
+      for (int b = SYM_FUSED_LAST + 1; b < NSMALL; ++b) fh += sb.flops[b];
+      for (int b = NSMALL; b < NSMALL + NGCLS; ++b) fb += sb.flops[b];
+      std::fprintf(stderr,
+                   "[cbg bins] fused cols %d flops %llu | hash cols %d flops %llu | big cols %d flops %llu | "
+                   "thin cols %d entries %lld flops %llu | inline A %d\n",
+                   sb.offset[SYM_FUSED_LAST + 1] - sb.offset[1], fs, sb.offset[NSMALL] - sb.offset[SYM_FUSED_LAST + 1],
+                   fh, nbig, fb, thin_R ? sb.count[THIN_BIN] : 0, (long long)thin_entries,
+                   thin_R ? (unsigned long long)sb.flops[THIN_BIN] : 0ull, ainl.p != nullptr);
+    }
+  }
   if (thin_R && sb.count[THIN_BIN] > 0)
     thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
                  B, cmap.p, ainl.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
