@@ -67,21 +67,29 @@ __global__ void k_colmap(int64_t nzc, const int64_t* __restrict__ cp, const int3
   }
 }
 
-// A's columns as inline records for the small-column passes (INL): x = length,
-// y = the row of a one-entry column, else its start, zw = that entry's value
+// A's columns as inline records for the small-column passes (INL), two int4 per
+// column: [2k] = {length, the first row (<= 2 entries) or the start, the second
+// row, 0}, [2k+1] = the one or two values (a 32-byte record: one line)
 __global__ void k_inline_cols(int64_t n1, const int2* __restrict__ cmap, const int32_t* __restrict__ irA,
                               const double* __restrict__ valA, int4* __restrict__ ainl) {
   const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (k >= n1) return;
   const int2 m = cmap[k];
-  int4 r = make_int4(m.y, m.x, 0, 0);
-  if (m.y == 1) {
-    const long long b = __double_as_longlong(valA[m.x]);
+  int4 r = make_int4(m.y, m.x, 0, 0), v = make_int4(0, 0, 0, 0);
+  if (m.y >= 1 && m.y <= 2) {
+    const long long b0 = __double_as_longlong(valA[m.x]);
     r.y = irA[m.x];
-    r.z = (int)b;
-    r.w = (int)(b >> 32);
+    v.x = (int)b0;
+    v.y = (int)(b0 >> 32);
+    if (m.y == 2) {
+      const long long b1 = __double_as_longlong(valA[m.x + 1]);
+      r.z = irA[m.x + 1];
+      v.z = (int)b1;
+      v.w = (int)(b1 >> 32);
+    }
   }
-  ainl[k] = r;
+  ainl[2 * k] = r;
+  ainl[2 * k + 1] = v;
 }
 
 // flops of every B column: FLOP_G lanes per column (B columns are short on
@@ -1501,10 +1509,10 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// INL: A's columns as inline records (k_inline_cols): {len, row of the only
-// entry or the start, the only entry's value}; a product of a one-entry A
-// column takes its row and value from the B entry's lane (shuffles) instead of
-// two random gathers -- GalerkinNew's S = T^T, Poisson(1) entries per column
+// INL: A's columns as inline records (k_inline_cols); a product of an A column
+// of one or two entries takes its row and value from the B entry's lane
+// (shuffles) instead of two random gathers -- GalerkinNew's S = T^T, Poisson(1)
+// entries per column
 template <int CPW, int NPL, int SR, bool INL>
 __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ perm, int n, int fmax,
                                                   const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
@@ -1547,15 +1555,18 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
     for (int cc = 1; cc < CPW; ++cc) c += __builtin_amdgcn_readlane(bexc, cc) <= e ? 1 : 0;
     const int ex_c = __shfl(bexc, c);
     const int64_t p0_c = __shfl(p0, c);
-    int s = 0, len = 0;
-    double bv = 0.0, v0 = 0.0;
+    int s = 0, len = 0, r1 = 0;
+    double bv = 0.0, v0 = 0.0, v1 = 0.0;
     if (e < totalB) {
       const int64_t p = p0_c + (e - ex_c);
       if constexpr (INL) {
-        const int4 r = ainl[irB[p]];
+        const int k = irB[p];
+        const int4 r = ainl[2 * (int64_t)k], v = ainl[2 * (int64_t)k + 1];
         len = r.x;
         s = r.y;
-        v0 = __hiloint2double(r.w, r.z);
+        r1 = r.z;
+        v0 = __hiloint2double(v.y, v.x);
+        v1 = __hiloint2double(v.w, v.z);
       } else {
         const int2 m = cmap[irB[p]];
         s = m.x;
@@ -1582,16 +1593,20 @@ __global__ __launch_bounds__(256) void k_esc_wave(const int32_t* __restrict__ pe
       const int o = lo;
       const int o_s = __shfl(s, o), o_ex = __shfl(pincl - len, o), o_c = __shfl(c, o);
       const double o_bv = __shfl(bv, o);
-      bool one = false;
-      double o_v0 = 0.0;
+      bool inl = false, second = false;
+      int o_r1 = 0;
+      double o_v0 = 0.0, o_v1 = 0.0;
       if constexpr (INL) {
-        one = __shfl(len, o) == 1;
+        inl = __shfl(len, o) <= 2;
+        second = q - o_ex == 1;
+        o_r1 = __shfl(r1, o);
         o_v0 = __shfl(v0, o);
+        o_v1 = __shfl(v1, o);
       }
       if (q >= 0 && q < ptot) {
-        if (INL && one) {
-          key[j] = (o_c << SH) | o_s;
-          val[j] = Sem<SR>::mul(o_v0, o_bv);
+        if (INL && inl) {
+          key[j] = (o_c << SH) | (second ? o_r1 : o_s);
+          val[j] = Sem<SR>::mul(second ? o_v1 : o_v0, o_bv);
         } else {
           const int a = o_s + (q - o_ex);
           key[j] = (o_c << SH) | irA[a];
@@ -3042,7 +3057,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     for (int b = 1; b < NSMALL; ++b) fsmall += sb.flops[b];
     fsmall += thin_R ? sb.flops[THIN_BIN] : 0;
     if (ainl_on && fused && A.nnz <= 2 * A.nzc && (double)fsmall >= 4.0 * (double)A.nnz) {
-      ainl.reset(A.n + 1);
+      ainl.reset(2 * (A.n + 1));
       hipLaunchKernelGGL(k_inline_cols, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, A.ir, A.val,
                          ainl.p);
     }

@@ -46,12 +46,12 @@ __global__ void k_thin_entries(const int32_t* __restrict__ perm, int n, const in
   const int64_t p = cpB[perm[lo]] + (e - eoff[lo]);
   ecol[e] = lo;
   epos[e] = p;
-  elen[e] = ainl ? ainl[irB[p]].x : cmap[irB[p]].y;
+  elen[e] = ainl ? ainl[2 * (int64_t)irB[p]].x : cmap[irB[p]].y;
 }
 
 // a wave per 64 flattened entries: their products, one per lane per round,
 // from the wave's first output position poff[e0]
-// INL: a one-entry A column's row and value come from the entry's lane (k_inline_cols)
+// INL: the rows and values of an A column of one or two entries come from the entry's lane (k_inline_cols)
 template <typename K, int SR, bool INL>
 __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* __restrict__ ecol,
                                                      const int64_t* __restrict__ epos,
@@ -64,15 +64,18 @@ __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* _
   if (e0 >= E) return;
   const int lane = lane_id();
   const int64_t e = e0 + lane;
-  int s = 0, len = 0, c = 0;
-  double bv = 0.0, v0 = 0.0;
+  int s = 0, len = 0, c = 0, r1 = 0;
+  double bv = 0.0, v0 = 0.0, v1 = 0.0;
   if (e < E) {
     const int64_t p = epos[e];
     if constexpr (INL) {
-      const int4 r = ainl[irB[p]];
+      const int k = irB[p];
+      const int4 r = ainl[2 * (int64_t)k], v = ainl[2 * (int64_t)k + 1];
       len = r.x;
       s = r.y;
-      v0 = __hiloint2double(r.w, r.z);
+      r1 = r.z;
+      v0 = __hiloint2double(v.y, v.x);
+      v1 = __hiloint2double(v.w, v.z);
     } else {
       const int2 m = cmap[irB[p]];
       s = m.x;
@@ -95,16 +98,20 @@ __global__ __launch_bounds__(256) void k_thin_expand(int64_t E, const int32_t* _
     }
     const int e_s = __shfl(s, lo), e_ex = __shfl(incl - len, lo), e_c = __shfl(c, lo);
     const double e_bv = __shfl(bv, lo);
-    bool one = false;
-    double e_v0 = 0.0;
+    bool inl = false, second = false;
+    int e_r1 = 0;
+    double e_v0 = 0.0, e_v1 = 0.0;
     if constexpr (INL) {
-      one = __shfl(len, lo) == 1;
+      inl = __shfl(len, lo) <= 2;
+      second = q - e_ex == 1;
+      e_r1 = __shfl(r1, lo);
       e_v0 = __shfl(v0, lo);
+      e_v1 = __shfl(v1, lo);
     }
     if (q < total) {
-      if (INL && one) {
-        keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)e_s;
-        vals[o + q] = Sem<SR>::mul(e_v0, e_bv);
+      if (INL && inl) {
+        keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)(second ? e_r1 : e_s);
+        vals[o + q] = Sem<SR>::mul(second ? e_v1 : e_v0, e_bv);
       } else {
         const int a = e_s + (q - e_ex);
         keys[o + q] = ((K)e_c << rowbits) | (K)(unsigned)irA[a];
