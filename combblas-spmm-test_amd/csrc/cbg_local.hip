@@ -509,13 +509,19 @@ __global__ __launch_bounds__(256) void k_sym_wave(const int32_t* __restrict__ pe
 template <int LOGT, int BS>
 struct SymBlockLds {
   static constexpr int T = 1 << LOGT;
-  static constexpr int INTS = T + (BS + 4) + BS + (BS / WAVE + 8);
+  static constexpr int INTS = T + (BS + 4) + BS + (BS / WAVE + 8) + 2 * BS;  // + inline first-product index, 2nd row
+};
+// a staged segment of an inline-record A column (INL): rows of the one or two
+// entries (ex = the segment's first product, -1: rows in irA)
+struct SegIL {
+  int off, ex, r1;
 };
 
-template <int LOGT, int BS>
+template <int LOGT, int BS, bool INL>
 __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ perm, const int64_t* __restrict__ cpB,
                                                   const int32_t* __restrict__ irB, const int2* __restrict__ cmap,
-                                                  const int32_t* __restrict__ irA, int32_t* __restrict__ cnt) {
+                                                  const int4* __restrict__ ainl, const int32_t* __restrict__ irA,
+                                                  int32_t* __restrict__ cnt) {
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* keys = reinterpret_cast<int*>(smem);
@@ -523,6 +529,8 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
   int* st = pref + BS + 4;
   int* tmp = st + BS;
   int& s_count = tmp[BS / WAVE + 4];  // outside block_excl_scan's scratch
+  int* sx = tmp + BS / WAVE + 8;  // INL: inline segment's first product (-1: none)
+  int* sr1 = sx + BS;             // INL: its second row
   const int tid = threadIdx.x;
   const int col = perm[blockIdx.x];
   for (int j = tid; j < T; j += BS) keys[j] = EMPTY_KEY;
@@ -532,24 +540,40 @@ __global__ __launch_bounds__(BS) void k_sym_block(const int32_t* __restrict__ pe
   int count = 0;
   for (int64_t c0 = cpB[col]; c0 < p1; c0 += BS) {
     const int64_t p = c0 + tid;
-    int s = 0, len = 0;
+    int s = 0, len = 0, r1 = 0;
     if (p < p1) {
-      int2 e = cmap[irB[p]];
-      s = e.x;
-      len = e.y;
+      if constexpr (INL) {
+        const int4 r = ainl[2 * (int64_t)irB[p]];
+        len = r.x;
+        s = r.y;
+        r1 = r.z;
+      } else {
+        int2 e = cmap[irB[p]];
+        s = e.x;
+        len = e.y;
+      }
     }
     int total;
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = seg_stage(s, ex);
+    if constexpr (INL) {
+      sx[tid] = len <= 2 ? ex : -1;
+      sr1[tid] = r1;
+    }
     __syncthreads();
-    block_products<BS>(
-        pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
-        [&](const SegI& g, int u) { return irA[g.off + u]; },
-        [&](int row) {
-          count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row);
-        });
+    if constexpr (INL) {
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegIL{seg_off(st, pref, sg), sx[sg], sr1[sg]}; },
+          [&](const SegIL& g, int u) { return g.ex < 0 ? irA[g.off + u] : u == g.ex ? g.off + u : g.r1; },
+          [&](int row) { count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row); });
+    } else {
+      block_products<BS>(
+          pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
+          [&](const SegI& g, int u) { return irA[g.off + u]; },
+          [&](int row) { count += hash_claim(keys, hash_slot<LOGT>(row), T - 1, row); });
+    }
     __syncthreads();
   }
   count = wave_sum(count);
@@ -2406,12 +2430,19 @@ static void launch_esc(const int32_t* perm, int n, int fmax, const cbg_tile& B, 
 #undef CBG_ESC_ARGS
 }
 template <int LOGT, int BS>
-static void launch_sym_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
-                             int32_t* cnt, hipStream_t s) {
+static void launch_sym_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const int4* ainl,
+                             const cbg_tile& A, int32_t* cnt, hipStream_t s) {
   if (n <= 0) return;
   const size_t lds = SymBlockLds<LOGT, BS>::INTS * sizeof(int);
-  set_lds(k_sym_block<LOGT, BS>, lds);
-  hipLaunchKernelGGL((k_sym_block<LOGT, BS>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, cmap, A.ir, cnt);
+  if (ainl) {
+    set_lds(k_sym_block<LOGT, BS, true>, lds);
+    hipLaunchKernelGGL((k_sym_block<LOGT, BS, true>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, cmap, ainl, A.ir,
+                       cnt);
+  } else {
+    set_lds(k_sym_block<LOGT, BS, false>, lds);
+    hipLaunchKernelGGL((k_sym_block<LOGT, BS, false>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, cmap, ainl, A.ir,
+                       cnt);
+  }
 }
 template <int LOGT, int SR>
 static void launch_num_wave(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
@@ -3100,9 +3131,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     }
     static_assert(SYM_FUSED_LAST == 8 || SYM_FUSED_LAST == 9, "fused bins");
     if (!fused || SYM_FUSED_LAST < 9) launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
-    launch_sym_block<11, 256>(at(10), sb.count[10], B, cmap.p, A, cnt.p, symst[10]);
-    launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, A, cnt.p, symst[11]);
-    launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, A, cnt.p, symst[12]);
+    launch_sym_block<11, 256>(at(10), sb.count[10], B, cmap.p, ainl.p, A, cnt.p, symst[10]);
+    launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, ainl.p, A, cnt.p, symst[11]);
+    launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, ainl.p, A, cnt.p, symst[12]);
   }
   bp.nbig = sb.offset[NSMALL + NGCLS] - sb.offset[NSMALL];
   bp.perm_big = sb.perm.p + sb.offset[NSMALL];
