@@ -13,7 +13,6 @@
 // one thread generates one edge; skip-ahead uses per-byte tables of powers of
 // the 5x5 MRG transition matrix, built on the host by square-and-multiply
 // (the role of the generated mrg_transitions.c table).
-#include <hipcub/hipcub.hpp>
 
 #include "cbg_device.h"
 #include "cbg_internal.h"
@@ -125,10 +124,21 @@ struct RmatParams {
   int scale;
   int pr, pc, prow, pcol;
   int64_t mper, nper;
+  unsigned long long drop_key;  // key of a dropped edge (loop / other tile): sorts last
 };
+// mask of the bits of values in [0, maxval]
+static unsigned long long rmat_bits(unsigned long long maxval) {
+  unsigned long long m = 0;
+  while (m < maxval) m = (m << 1) | 1ull;
+  return m;
+}
 
+// keys of this tile's edges, appended in any order (the sort follows); dropped
+// edges (loops, other tiles) are not written -- 7/8 of a 2x4 grid's edges,
+// whose one long run of equal keys would serialize a reduce-by-key thread
 __global__ __launch_bounds__(256) void k_rmat_edges(int64_t e0, int64_t ne, const uint32_t* __restrict__ tab,
-                                                    RmatParams P, unsigned long long* __restrict__ keys) {
+                                                    RmatParams P, unsigned long long* __restrict__ keys,
+                                                    unsigned long long* __restrict__ nkept) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= ne) return;
   const uint64_t ei = (uint64_t)(e0 + t);
@@ -183,7 +193,7 @@ __global__ __launch_bounds__(256) void k_rmat_edges(int64_t e0, int64_t ne, cons
   }
   const int64_t src = scramble_d(bs, P.scale, P.val0, P.val1);
   const int64_t dst = scramble_d(bt, P.scale, P.val0, P.val1);
-  unsigned long long key = ~0ULL;
+  unsigned long long key = P.drop_key;  // sorts after every kept edge
   if (src != dst) {  // RemoveLoops
     const int orow = P.mper ? (int)min(src / P.mper, (int64_t)P.pr - 1) : P.pr - 1;
     const int ocol = P.nper ? (int)min(dst / P.nper, (int64_t)P.pc - 1) : P.pc - 1;
@@ -192,20 +202,32 @@ __global__ __launch_bounds__(256) void k_rmat_edges(int64_t e0, int64_t ne, cons
       key = (lc << 32) | lr;
     }
   }
-  keys[t] = key;
+  const bool kept = key != P.drop_key;
+  const unsigned long long m = __ballot(kept);  // one atomic per wave
+  if (m) {
+    const int lane = lane_id(), leader = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(nkept, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (kept) keys[base + __popcll(m & ((1ull << lane) - 1ull))] = key;
+  }
 }
 
 __global__ void k_rmat_flags(int64_t n, const unsigned long long* __restrict__ uk, int64_t* __restrict__ flag) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) flag[i] = (i == 0 || (uk[i] >> 32) != (uk[i - 1] >> 32)) ? 1 : 0;
 }
-__global__ void k_rmat_fill(int64_t n, const unsigned long long* __restrict__ uk, const int* __restrict__ cnt,
+__global__ void k_ones(int64_t n, double* __restrict__ v) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) v[i] = 1.0;
+}
+__global__ void k_rmat_fill(int64_t n, const unsigned long long* __restrict__ uk, const double* __restrict__ cnt,
                             const int64_t* __restrict__ pos, int32_t* __restrict__ ir, double* __restrict__ val,
                             int32_t* __restrict__ jc, int64_t* __restrict__ cp) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   ir[i] = (int32_t)(uk[i] & 0xFFFFFFFFULL);
-  val[i] = (double)cnt[i];  // multiplicity of the edge (SpTuples.cpp:95-101)
+  val[i] = cnt[i];  // multiplicity of the edge (SpTuples.cpp:95-101)
   if (i == 0 || (uk[i] >> 32) != (uk[i - 1] >> 32)) {
     jc[pos[i]] = (int32_t)(uk[i] >> 32);
     cp[pos[i]] = i;
@@ -238,43 +260,41 @@ void rmat_tile(int scale, int ef, uint64_t userseed, int pr, int pc, int prow, i
   P.mper = nv / pr;
   P.nper = nv / pc;
   const int64_t M = nv * ef;
-  // hipcub's sort / run-length encode count items in int: 2^scale * ef < 2^31
-  // (scale 26 at ef 16; the configurations stop at 24)
-  if (M >= (int64_t)INT32_MAX) throw HipError("R-MAT generator: 2^scale * edgefactor must stay below 2^31", CBG_ERR_NOTSUPPORTED);
   const int64_t lm = (prow == pr - 1) ? nv - prow * P.mper : P.mper;
   const int64_t ln = (pcol == pc - 1) ? nv - pcol * P.nper : P.nper;
+  // keys (local col << 32 | local row); dropped edges (loops, other tiles) get
+  // column ln, one past the tile, so they sort last; the radix sort only runs
+  // over the bits these keys can use
+  P.drop_key = (unsigned long long)ln << 32;
+  const unsigned long long varying = (rmat_bits((unsigned long long)ln) << 32) | rmat_bits((unsigned long long)(lm - 1));
 
-  DBuf<unsigned long long> k0(M), k1(M);
-  hipLaunchKernelGGL(k_rmat_edges, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (int64_t)0, M, tb.dev, P, k0.p);
-  size_t tmp_bytes = 0;
-  CBG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp_bytes, k0.p, k1.p, (int)M, 0, 64, s));
-  DBuf<char> tmp(tmp_bytes);
-  CBG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tmp_bytes, k0.p, k1.p, (int)M, 0, 64, s));
-  // run-length encode: unique (col,row) and multiplicities
-  DBuf<int> cnt(M);
-  DBuf<int> nruns(1);
-  size_t tb2 = 0;
-  CBG_HIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb2, k1.p, k0.p, cnt.p, nruns.p, (int)M, s));
-  DBuf<char> tmp2(tb2);
-  CBG_HIP(hipcub::DeviceRunLengthEncode::Encode(tmp2.p, tb2, k1.p, k0.p, cnt.p, nruns.p, (int)M, s));
-  int runs = 0;
-  CBG_HIP(hipMemcpyAsync(&runs, nruns.p, sizeof(int), hipMemcpyDeviceToHost, s));
-  unsigned long long last = 0;
+  // edges -> (key, 1.0); sort; duplicates summed = the multiplicities
+  // (cbg_sort.hip: the repo's radix sort and reduce-by-key, 64-bit counts)
+  DBuf<unsigned long long> k0(M), nk(1);
+  CBG_HIP(hipMemsetAsync(nk.p, 0, sizeof(unsigned long long), s));
+  hipLaunchKernelGGL(k_rmat_edges, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (int64_t)0, M, tb.dev, P, k0.p,
+                     nk.p);
+  unsigned long long kept = 0;
+  CBG_HIP(hipMemcpyAsync(&kept, nk.p, sizeof(kept), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipStreamSynchronize(s));
-  if (runs > 0) {
-    CBG_HIP(hipMemcpy(&last, k0.p + runs - 1, sizeof(last), hipMemcpyDeviceToHost));
-    if (last == ~0ULL) --runs;  // dropped edges (loops, other tiles) sort last
-  }
+  const int64_t E = (int64_t)kept;
+  DBuf<unsigned long long> uk(std::max<int64_t>(E, 1));
+  DBuf<double> w0(std::max<int64_t>(E, 1)), uv(std::max<int64_t>(E, 1));
+  if (E > 0) hipLaunchKernelGGL(k_ones, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, s, E, w0.p);
+  radix_sort_pairs<unsigned long long>(k0, w0, E, varying, s);
+  const int64_t runs = reduce_by_key<unsigned long long>(k0.p, w0.p, E, CBG_PLUS_TIMES, uk.p, uv.p, s);
+  k0.release();
+  w0.release();
   const int64_t nnz = runs;
   DBuf<int64_t> flag(nnz + 1), pos(nnz + 1);
-  hipLaunchKernelGGL(k_rmat_flags, dim3((unsigned)((nnz + 255) / 256 + 1)), dim3(256), 0, s, nnz, k0.p, flag.p);
+  hipLaunchKernelGGL(k_rmat_flags, dim3((unsigned)((nnz + 255) / 256 + 1)), dim3(256), 0, s, nnz, uk.p, flag.p);
   exclusive_scan_i64(flag.p, pos.p, nnz, s);
   int64_t nzc = 0;
   CBG_HIP(hipMemcpyAsync(&nzc, pos.p + nnz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipStreamSynchronize(s));
   tile_alloc_device(out, lm, ln, nnz, nzc);
   if (nnz > 0)
-    hipLaunchKernelGGL(k_rmat_fill, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, k0.p, cnt.p, pos.p,
+    hipLaunchKernelGGL(k_rmat_fill, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, nnz, uk.p, uv.p, pos.p,
                        out.ir, out.val, out.jc, out.cp);
   CBG_HIP(hipMemcpyAsync(out.cp + nzc, &nnz, sizeof(int64_t), hipMemcpyHostToDevice, s));
   CBG_HIP(hipStreamSynchronize(s));
