@@ -314,8 +314,11 @@ constexpr int BIN_ITEMS = 16;
 // thin_R > 0: big columns with flops * THIN_RATIO < B entries * thin_R go to
 // thin_bin (mode 0) / are skipped like the fused ones (mode 1)
 constexpr int64_t THIN_RATIO = 4;
+// copy1: a column with one B entry and 0 < flops <= big is C(:,j) = A(:,k) * b,
+// nnz = flops: mode 0 writes cnt and bins it with the empty columns, mode 1
+// skips it (k_copy_single writes it)
 __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __restrict__ flops,
-                                                  const int32_t* __restrict__ cnt, int mode, int64_t big, BinThr thr,
+                                                  int32_t* __restrict__ cnt, int mode, int copy1, int64_t big, BinThr thr,
                                                   uint8_t* __restrict__ bin, int* __restrict__ hist,
                                                   int64_t fused_max, const int64_t* __restrict__ cpB, int big_bin,
                                                   unsigned long long* __restrict__ big_entries,
@@ -341,13 +344,19 @@ __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __re
       // thin big columns (cbg_thin.hip): few products per B entry, so the R
       // (column, panel) pairs would each stage the whole column for little
       const bool thin = thin_R > 0 && f > big && f * THIN_RATIO < (cpB[i + 1] - cpB[i]) * (int64_t)thin_R;
+      const bool single = copy1 && f > 0 && f <= big && cpB[i + 1] - cpB[i] == 1;
       // numeric bins: big columns last; columns computed by the fused small-column
-      // pass (0 < flops <= fused_max) or the thin pass in bin 0, which the numeric skips
-      if (mode == 1) key = thin ? 0 : (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
+      // pass (0 < flops <= fused_max), the thin pass or the single-entry copy in
+      // bin 0, which the numeric skips
+      if (mode == 1) key = (thin || single) ? 0 : (key > big) ? INT64_MAX : (key <= fused_max) ? 0 : (int64_t)cnt[i];
       int b = thr.nb - 1;
       for (int q = 0; q < thr.nb - 1; ++q)
         if (key <= thr.t[q]) { b = q; break; }
       if (mode == 0 && thin) b = thin_bin;
+      if (single) {
+        b = 0;
+        if (mode == 0) cnt[i] = (int32_t)f;
+      }
       bin[i] = (uint8_t)b;
       atomicAdd(&lh[b], 1);
       if (f > 0) atomicAdd(&lf[b], (unsigned long long)f);
@@ -1746,6 +1755,53 @@ __global__ __launch_bounds__(256) void k_copy_fused(int64_t nz, const int64_t* _
   }
 }
 
+// single-entry columns (k_classify copy1): C(:,j) = A(:,k) * b, flattened per
+// wave along C like k_copy_fused (rows are A's, already ascending)
+template <int SR>
+__global__ __launch_bounds__(256) void k_copy_single(int64_t nz, const int64_t* __restrict__ cpB,
+                                                     const int32_t* __restrict__ irB, const double* __restrict__ valB,
+                                                     const int2* __restrict__ cmap, const int64_t* __restrict__ flops,
+                                                     int64_t big, const int32_t* __restrict__ irA,
+                                                     const double* __restrict__ valA, const int64_t* __restrict__ colptr,
+                                                     int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
+  const int64_t c0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE * WAVE;
+  if (c0 >= nz) return;
+  const int lane = lane_id();
+  const int64_t col = c0 + lane;
+  int64_t dst = 0;
+  int src = 0, c = 0;
+  double b = 0.0;
+  if (col < nz) {
+    const int64_t p = cpB[col], f = flops[col];
+    if (cpB[col + 1] - p == 1 && f > 0 && f <= big) {
+      const int2 m = cmap[irB[p]];
+      src = m.x;
+      c = m.y;
+      b = valB[p];
+      dst = colptr[col];
+    }
+  }
+  const int incl = wave_incl_scan(c);
+  const int total = wave_last(incl);
+  for (int q0 = 0; q0 < total; q0 += WAVE) {
+    const int q = q0 + lane;
+    int lo = 0, hi = WAVE - 1;  // the column of flattened entry q
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const int mid = (lo + hi) >> 1;
+      if (__shfl(incl, mid) > q) hi = mid; else lo = mid + 1;
+    }
+    const int o_src = __shfl(src, lo), o_ex = __shfl(incl - c, lo);
+    const int64_t o_dst = __shfl(dst, lo);
+    const double o_b = __shfl(b, lo);
+    if (q < total) {
+      const int e = q - o_ex;
+      out_ir[o_dst + e] = irA[o_src + e];
+      out_val[o_dst + e] = Sem<SR>::mul(valA[o_src + e], o_b);
+    }
+  }
+}
+
 // numeric: block per column
 template <int LOGT, int BS>
 struct NumBlockLds {
@@ -2680,9 +2736,10 @@ struct BinPending {
   }
 };
 // cpB/big_bin (mode 0): also count the B entries of the bins >= big_bin into bp.big_entries
-static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, int mode, const int64_t* thr,
+static void bin_classify(int64_t n, const int64_t* flops, int32_t* cnt, int mode, const int64_t* thr,
                          int nthr, int64_t big, BinPending& bp, hipStream_t s, int64_t fused_max = 0,
-                         const int64_t* cpB = nullptr, int big_bin = MAXBINS, int thin_R = 0, int thin_bin = 0) {
+                         const int64_t* cpB = nullptr, int big_bin = MAXBINS, int thin_R = 0, int thin_bin = 0,
+                         int copy1 = 0) {
   bp.bt.nb = nthr + 1;
   for (int i = 0; i < nthr; ++i) bp.bt.t[i] = thr[i];
   bp.bin.reset(n);
@@ -2691,7 +2748,7 @@ static void bin_classify(int64_t n, const int64_t* flops, const int32_t* cnt, in
   CBG_HIP(hipMemsetAsync(bp.hist.p, 0, sizeof(int) * (4 * MAXBINS + 4), s));
   unsigned long long* be = (cpB && mode == 0) ? reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS) : nullptr;
   unsigned long long* bf = reinterpret_cast<unsigned long long*>(bp.hist.p + 2 * MAXBINS + 4);
-  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, flops, cnt, mode, big, bp.bt,
+  hipLaunchKernelGGL(k_classify, dim3(nblk(n, 256 * BIN_ITEMS)), dim3(256), 0, s, n, flops, cnt, mode, copy1, big, bp.bt,
                      bp.bin.p, bp.hist.p, fused_max, cpB, big_bin, be, bf, thin_R, thin_bin);
   // one copy of counts | offsets | big entries | flops per bin
   bp.host = host_stage(mode == 0 ? STAGE_BINS_SYM : STAGE_BINS_NUM);
@@ -3025,6 +3082,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // small columns' symbolic and numeric in one pass (bins 1..SYM_FUSED_LAST), unless CBG_FUSE_SMALL=0
   static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
   const bool fused = fuse_small;
+  // single-entry columns as scaled copies of A's columns (CBG_COPY1=0: off)
+  static const int copy1 = (getenv("CBG_COPY1") && !strcmp(getenv("CBG_COPY1"), "0")) ? 0 : 1;
   bp.plog = pick_panel_log(A.m);
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
   constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1, THIN_BIN = NSMALL + NGCLS;
@@ -3050,14 +3109,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const char* tr = getenv("CBG_THIN_RATIO");
     const int ratio = tr ? std::max(1, atoi(tr)) : (int)THIN_RATIO;
     thin_R = (fused && thin_on && bp.R >= 4) ? (int)(bp.R * THIN_RATIO / ratio) : 0;
-    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN);
+    bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN, copy1);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
     sp.read();
     if (thin_R && (double)sp.hf[THIN_BIN] * THIN_BYTES_PER_PRODUCT > 0.25 * device_bytes_available()) {
       // the sort's temporaries (64-bit counts, cbg_sort.hip) would take more than a
       // quarter of the device memory left: classify again without thin columns
       thin_R = 0;
-      bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, 0, THIN_BIN);
+      bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, 0, THIN_BIN, copy1);
       CBG_HIP(hipStreamSynchronize(s));
       sp.read();
     }
@@ -3272,7 +3331,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   BinPending npend;
   bin_classify(nz, flops.p, cnt.p, 1, kNumThr, 9, big, npend, s, fused ? kSymThr[SYM_FUSED_LAST] : 0, B.cp,
-               MAXBINS, thin_R, 0);
+               MAXBINS, thin_R, 0, copy1);
   // compaction of C's columns (SpDCCols(SpTuples): nonempty columns only)
   DBuf<int64_t> flag(nz + 1), pos(nz + 1);
   hipLaunchKernelGGL(k_col_flags, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, cnt.p, flag.p);
@@ -3390,6 +3449,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (thin_R)
       thin_copy(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], fused_slot.p, cnt.p, colptr.p, fused_ir.p,
                 fused_val.p, C.ir, C.val, s);
+  }
+  if (copy1) {
+    if (semiring == CBG_MIN_PLUS)
+      hipLaunchKernelGGL(k_copy_single<1>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
+                         flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
+    else
+      hipLaunchKernelGGL(k_copy_single<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
+                         flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
