@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t n, const int64_t* __re
       // thin big columns (cbg_thin.hip): few products per B entry, so the R
       // (column, panel) pairs would each stage the whole column for little
       const bool thin = thin_R > 0 && f > big && f * THIN_RATIO < (cpB[i + 1] - cpB[i]) * (int64_t)thin_R;
-      const bool single = copy1 && f > 0 && f <= big && cpB[i + 1] - cpB[i] == 1;
+      const bool single = copy1 && f > 0 && (f <= big || copy1 > 1) && cpB[i + 1] - cpB[i] == 1;
       // numeric bins: big columns last; columns computed by the fused small-column
       // pass (0 < flops <= fused_max), the thin pass or the single-entry copy in
       // bin 0, which the numeric skips
@@ -1755,7 +1755,7 @@ __global__ __launch_bounds__(256) void k_copy_fused(int64_t nz, const int64_t* _
   }
 }
 
-// single-entry columns (k_classify copy1): C(:,j) = A(:,k) * b, flattened per
+// single-entry columns of <= big flops (k_classify copy1): C(:,j) = A(:,k) * b, flattened per
 // wave along C like k_copy_fused (rows are A's, already ascending)
 template <int SR>
 __global__ __launch_bounds__(256) void k_copy_single(int64_t nz, const int64_t* __restrict__ cpB,
@@ -1798,6 +1798,36 @@ __global__ __launch_bounds__(256) void k_copy_single(int64_t nz, const int64_t* 
       const int e = q - o_ex;
       out_ir[o_dst + e] = irA[o_src + e];
       out_val[o_dst + e] = Sem<SR>::mul(valA[o_src + e], o_b);
+    }
+  }
+}
+
+// the single-entry columns of more than `big` flops (copy1 = 2): a block takes
+// 256 columns and copies each such column with all its threads
+template <int SR>
+__global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64_t* __restrict__ cpB,
+                                                         const int32_t* __restrict__ irB,
+                                                         const double* __restrict__ valB,
+                                                         const int2* __restrict__ cmap,
+                                                         const int64_t* __restrict__ flops, int64_t big,
+                                                         const int32_t* __restrict__ irA,
+                                                         const double* __restrict__ valA,
+                                                         const int64_t* __restrict__ colptr,
+                                                         int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
+  __shared__ int64_t list[256];
+  __shared__ int nlist;
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (col < nz && flops[col] > big && cpB[col + 1] - cpB[col] == 1) list[atomicAdd(&nlist, 1)] = col;
+  __syncthreads();
+  for (int l = 0; l < nlist; ++l) {
+    const int64_t c = list[l], p = cpB[c], dst = colptr[c];
+    const int2 m = cmap[irB[p]];
+    const double b = valB[p];
+    for (int e = threadIdx.x; e < m.y; e += blockDim.x) {
+      out_ir[dst + e] = irA[m.x + e];
+      out_val[dst + e] = Sem<SR>::mul(valA[m.x + e], b);
     }
   }
 }
@@ -3083,7 +3113,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
   const bool fused = fuse_small;
   // single-entry columns as scaled copies of A's columns (CBG_COPY1=0: off)
-  static const int copy1 = (getenv("CBG_COPY1") && !strcmp(getenv("CBG_COPY1"), "0")) ? 0 : 1;
+  // (default 2: also those of more than `big` flops -- R-MAT columns whose one
+  // entry hits a hub -- instead of (column, panel) pairs: s22 446.4 -> 440.9 ms;
+  // 1: only the small ones)
+  static const int copy1 = getenv("CBG_COPY1") ? atoi(getenv("CBG_COPY1")) : 2;
   bp.plog = pick_panel_log(A.m);
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
   constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1, THIN_BIN = NSMALL + NGCLS;
@@ -3457,6 +3490,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     else
       hipLaunchKernelGGL(k_copy_single<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
                          flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
+  }
+  if (copy1 > 1) {
+    if (semiring == CBG_MIN_PLUS)
+      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val,
+                         cmap.p, flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
+    else
+      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val,
+                         cmap.p, flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
