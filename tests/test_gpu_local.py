@@ -171,7 +171,7 @@ def test_thin_big_columns(cbg, sr):
     for L in lens:
         ir.extend(np.sort(rng.choice(k, int(L), replace=False)))
         cp.append(len(ir))
-    ir.extend([k])  # the hub column alone
+    ir.extend([0, k])  # the hub column and one short one: a regular big column (one entry alone is a copy)
     cp.append(len(ir))
     nB = len(cp) - 1
     Bh = dict(m=k + 1, n=nB, cp=np.array(cp, np.int64), jc=np.arange(nB, dtype=np.int32),
@@ -183,6 +183,45 @@ def test_thin_big_columns(cbg, sr):
     else:
         assert_tiles_equal(C, ref)
     assert cbg.last_stats()["n_big"] == 1  # the thin columns left the (column, panel) path
+
+
+@pytest.mark.parametrize("sr", ["plus", "minplus"])
+def test_single_entry_columns(cbg, sr):
+    """B columns with one entry are scaled copies of an A column (k_copy_single /
+    k_copy_single_big: no symbolic or hash work): short and hub A columns (above
+    the 4096-flop big threshold), zero and negative B values, next to ordinary
+    small and big columns; entry by entry against the oracle."""
+    rng = np.random.default_rng(5)
+    m, k = (1 << 19) + 11, 3000
+    lens = np.concatenate([rng.integers(0, 30, k - 6), [5000, 9000, 20000, 70000, 4096, 4097]]).astype(np.int64)
+    ir, cp = [], [0]
+    for L in lens:
+        ir.extend(np.sort(rng.choice(m, int(L), replace=False)))
+        cp.append(len(ir))
+    Ah = dict(m=m, n=k, cp=np.array(cp, np.int64), jc=np.arange(k, dtype=np.int32), ir=np.array(ir, np.int32),
+              val=rng.uniform(-2.0, 2.0, len(ir)))
+    bcols = []
+    for j in range(400):
+        t = j % 4
+        if t == 0:    # one entry: a short A column
+            bcols.append([int(rng.integers(0, k - 6))])
+        elif t == 1:  # one entry: a hub
+            bcols.append([int(k - 6 + rng.integers(0, 6))])
+        elif t == 2:  # a few short ones
+            bcols.append(sorted(rng.choice(k - 6, 5, replace=False).tolist()))
+        else:         # hubs and short ones: a big column
+            bcols.append(sorted(set(rng.choice(k - 6, 3, replace=False).tolist() + [k - 3, k - 2])))
+    cpB = np.cumsum([0] + [len(c) for c in bcols]).astype(np.int64)
+    irB = np.concatenate([np.array(c, np.int32) for c in bcols])
+    valB = rng.uniform(-1.0, 1.0, len(irB))
+    valB[::7] = 0.0  # explicit zero products stay structural entries
+    Bh = dict(m=k, n=len(bcols), cp=cpB, jc=np.arange(len(bcols), dtype=np.int32), ir=irB, val=valB)
+    C = cbg.LocalHybridSpGEMM(cbg.Tile.from_dict(Ah), cbg.Tile.from_dict(Bh), sr).to_host()
+    ref = oracle_local(Ah, Bh, sr)
+    if sr == "plus":
+        assert_tiles_equal(C, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+    else:
+        assert_tiles_equal(C, ref)
 
 
 def test_big_columns_tall_matrix(cbg):
