@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 4: few-entry big columns through the thin sort (CBG_FEW) -- parity subset,
+# GalerkinNew scale 22 on / off (3 rounds), the scale-22 bench on / off
+set -o pipefail
+out=gpurun_out/x
+mkdir -p $out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_local.py -x -q --timeout 300 --timeout-method thread -k "galerkin or thin or restriction or local_digest or single or panel_groups" > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+tail -1 $out/tests.log
+for r in 1 2 3; do
+  for f in 8 0; do
+    CBG_FEW=$f timeout -k 10 200 python tools/galerkin.py --scale 22 --iters 5 --only-full > $out/gal_${f}_$r.json 2>>$out/err.log || exit 1
+    python3 -c "import json;d=json.load(open('$out/gal_${f}_$r.json'));print('galerkin round $r few=$f', round(d['full_restriction_s']*1e3,3), 'ms')"
+  done
+done
+for f in 8 0; do
+  CBG_FEW=$f timeout -k 10 300 python bench.py --no-cpu-baseline --steps 5 --warmup 1 > $out/b_$f.json 2>>$out/err.log || exit 1
+  python3 -c "import json;d=json.load(open('$out/b_$f.json'));print('s22 few=$f', round(d['ms_per_step'],2), 'ms')"
+done
