@@ -3194,8 +3194,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     for (int b = NSMALL; b < NSMALL + NGCLS; ++b) main_w += (double)sb.flops[b];
     double cost[NSMALL];
     for (int b = 0; b < NSMALL; ++b) cost[b] = (fused && b >= 1 && b <= SYM_FUSED_LAST) ? 2.0 : 1.0;
-    symst[0] = ssym;
-    balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, ssym, symst);
+    // Without CBG_SIDE: the small symbolic bins join the main stream, ahead of
+    // the (column, panel) units, when those carry most of the flops over >= 8
+    // row panels -- on the side stream they co-ran with k_sym_panel for its
+    // whole length and slowed it (scale 22: 436.3 vs 443.1 ms, scale 24:
+    // 3948 vs 3965 ms); small products (scale 18: R = 1) and small-column
+    // products (GalerkinNew) keep the concurrency (side: 6.67 vs 6.79 ms and
+    // 6.37 vs 6.85 ms)
+    hipStream_t sy = ssym;
+    if (!getenv("CBG_SIDE") && bp.R >= 8) {
+      double small_w = 0.0;
+      for (int b = 1; b < NSMALL; ++b) small_w += (double)sb.flops[b];
+      if (main_w >= small_w) sy = s;
+    }
+    symst[0] = sy;
+    balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, sy, symst);
   }
   {
     const int32_t* P = sb.perm.p;
