@@ -3,16 +3,23 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--phases P]
                   [--algo doublebuff|synch] [--exec panel|staged] [--no-cpu-baseline]
+                  [--values rmat|random] [--no-f64-leg] [--grid RxC]
 
 One step = one complete Mult_AnXBn_DoubleBuff (reference ParFriends.h:798-997)
 of Graph500 R-MAT A (SEED 0xDECAFBAD, ef 16, duplicates summed, loops removed)
 by a deep copy of A, inputs resident in HBM in the 2D block layout.  Every N
 runs the metric's scale 22 as MemEfficientSpGEMM (ParFriends.h:449) whose
 phase count the library picks from device memory inside every step (N=1: C is
-297 GB, more than one GPU's HBM: 3 B-column phases, each phase's C
+297 GB, more than one GPU's HBM: 2 B-column phases of ~149 GB, each phase's C
 materialized in HBM and handed to the consumer; a C tile that fits runs as one
-phase, the adaptive double-buffered DoubleBuff).  N>1 is launched by torch.distributed.run, one rank per GPU, RCCL
-row/column communicators (grid 2x1, 2x2, 4x2 for 2/4/8).  --scale 18 gives
+phase, the adaptive double-buffered DoubleBuff).  N>1 is launched by
+torch.distributed.run, one rank per GPU, RCCL row/column communicators (grids
+2x1, 2x2, 4x2 for 2/4/8: DESIGN.md section 6 gives the measured reason; --grid
+1x2 / 2x4 runs BASELINE.md's shapes); an RCCL grid that cannot be created ends
+the run non-zero (CBG_ALLOW_HOST_TRANSPORT=1 opts into the TCP host transport).
+After the headline loop the same structure is timed again with f64 values
+(f64_values / roofline.frac_f64_values): R-MAT's integer values let the slab
+kernels read A as exact f32, real-valued matrices do not.  --scale 18 gives
 configs[1] (C resident on one GPU).
 
 Prints ONE JSON line on rank 0 (see the driver contract in DESIGN.md).
@@ -68,6 +75,8 @@ def parse():
                    help="rmat: the generator's duplicate counts (small integers); random: U[-1,1) from a hash of "
                         "(row, col) on the same structure (SURVEY 8(d)'s fp variant; A's values are then f64)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-f64-leg", dest="f64_leg", action="store_false",
+                   help="skip the second timed loop with f64 (random) values on the same structure")
     p.add_argument("--cpu-threads", type=int, default=0, help="default: the CPUs this job may use")
     p.add_argument("--cpu-scale", type=int, default=20, help="scale of the CPU-baseline sample (reference Synch)")
     return p.parse_args()
@@ -196,6 +205,74 @@ def cpu_baseline(scale, ef, seed, threads):
     return best
 
 
+def host_transport_fallback(rank, err, env=None):
+    """The RCCL grid could not be created.  An N>1 line measured over the TCP
+    host transport says nothing about RCCL over xGMI, so the bench exits
+    non-zero (the driver sees a failed run, not a socket number with rc 0)
+    unless the fallback is asked for explicitly: CBG_ALLOW_HOST_TRANSPORT=1
+    (development runs of the N>1 logic with several ranks on one GPU)."""
+    env = os.environ if env is None else env
+    if env.get("CBG_ALLOW_HOST_TRANSPORT") != "1":
+        raise SystemExit(f"[bench] rank {rank}: RCCL grid unavailable ({err}); not falling back to the TCP "
+                         "host transport (set CBG_ALLOW_HOST_TRANSPORT=1 to allow it)")
+    print(f"[bench] rank {rank}: RCCL grid unavailable ({err}); using the TCP host transport "
+          "(CBG_ALLOW_HOST_TRANSPORT=1)", file=sys.stderr, flush=True)
+
+
+def roofline_over_ranks(bytes_alg, ms_avg, n, peak_gbs):
+    """Roofline of the local multiplies of all ranks as one job: the bytes of
+    every rank's local multiply over the SLOWEST rank's device time, per GPU
+    (sum of bytes / max ms / N), so a fast rank cannot stand for the grid
+    (bytes_alg, ms_avg: per-rank lists).  Also the slowest rank's own rate."""
+    slow = max(range(n), key=lambda r: ms_avg[r])
+    achieved = sum(bytes_alg) / (ms_avg[slow] * 1e-3) / n / 1e9
+    slowest_rank = bytes_alg[slow] / (ms_avg[slow] * 1e-3) / 1e9
+    return {"achieved": achieved, "frac": achieved / peak_gbs, "slowest_rank": slow,
+            "slowest_rank_achieved": slowest_rank, "slowest_rank_frac": slowest_rank / peak_gbs}
+
+
+def f64_values_leg(cbg, grid, A, B, a, step, N):
+    """The same product with f64 values (U[-1,1) from a hash of (row, col), the
+    structure unchanged), timed like the headline: R-MAT's small-integer values
+    let the slab kernels read A's values as exact f32 (bit-identical results),
+    which real-valued matrices cannot.  Reported beside the headline (rmat
+    values only; --values random is this leg as the headline)."""
+    if a.values != "rmat":
+        return None
+    r0_ = cbg.block_range(1 << (a.scale if a.scale is not None else 22), grid.grid_rows, grid.prow)[0]
+    c0_ = cbg.block_range(1 << (a.scale if a.scale is not None else 22), grid.grid_cols, grid.pcol)[0]
+    A.tile.set_random_values(row_off=r0_, col_off=c0_)
+    B.tile.set_random_values(row_off=r0_, col_off=c0_)
+    cbg.synchronize()
+    for _ in range(a.warmup):
+        _, C = step()
+        if C is not None:
+            C.tile.free()
+    step_s, ms = [], []
+    for _ in range(a.steps):
+        grid.barrier()
+        ts = time.perf_counter()
+        _, C = step()
+        cbg.synchronize()
+        step_s.append(grid.allreduce_max(time.perf_counter() - ts))
+        if C is not None:
+            C.tile.free()
+        st = cbg.last_stats()
+        ms.append(st["ms_symbolic"] + st["ms_numeric"])
+    st = cbg.last_stats()
+    col_nnz = [grid.allreduce_sum(B.tile.nnz if grid.pcol == c else 0) for c in range(grid.grid_cols)]
+    bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * col_nnz[grid.pcol] + 8 * B.tile.n
+    ms_avg = sum(ms) / len(ms)
+    rank = grid.rank
+    ms_ranks = [grid.allreduce_max(ms_avg if r == rank else -1.0) for r in range(N)]
+    bytes_ranks = [grid.allreduce_sum(bytes_alg if r == rank else 0) for r in range(N)]
+    roof = roofline_over_ranks(bytes_ranks, ms_ranks, N, HBM_PEAK_GBS)
+    med = sorted(step_s)[len(step_s) // 2]
+    return {"values": "U[-1,1) from a hash of (row, col): A's values are f64 (no f32 narrowing)",
+            "ms_per_step": med * 1e3, "step_ms": [round(x * 1e3, 3) for x in step_s],
+            "achieved": roof["achieved"], "frac": roof["frac"], "ms_avg": ms_ranks[roof["slowest_rank"]]}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -253,13 +330,10 @@ def main():
             transport = "rccl (socket rehearsal: all ranks on one GPU)" if rehearsal else "rccl"
             hc.close()
         except cbg.CbgError as e:
-            # e.g. several ranks on one GPU (RCCL rejects duplicate devices): keep
-            # the SUMMA on the host transport so the run still completes
-            print(f"[bench] rank {rank}: RCCL grid unavailable ({e}); using the TCP host transport",
-                  file=sys.stderr, flush=True)
+            host_transport_fallback(rank, e)  # exits non-zero unless explicitly allowed
             hc.allgather(0, b"0")  # every rank agrees on the fallback
             grid = cbg.CommGrid(rank, N, pr, pc, transport="host", host_comm=hc)
-            transport = "host-tcp"
+            transport = "host-tcp (opt-in fallback: NOT an RCCL/xGMI number)"
 
     t_gen = time.perf_counter()
     A = cbg.SpParMat.rmat(grid, scale, a.ef, a.seed)
@@ -334,8 +408,19 @@ def main():
     col_nnz = [grid.allreduce_sum(B.tile.nnz if grid.pcol == c else 0) for c in range(pc)]
     bytes_alg = 16 * st["flops"] + 12 * st["nnz"] + 32 * col_nnz[grid.pcol] + 8 * B.tile.n
     ms_avg = sum(ms_local) / len(ms_local)
-    achieved = bytes_alg / (ms_avg * 1e-3) / 1e9
-    achieved = grid.allreduce_max(achieved) if N > 1 else achieved
+    # every rank's bytes and device ms (one max-reduction per rank: N <= 16)
+    ms_ranks = [grid.allreduce_max(ms_avg if r == rank else -1.0) for r in range(N)]
+    bytes_ranks = [grid.allreduce_sum(bytes_alg if r == rank else 0) for r in range(N)]
+    roof = roofline_over_ranks(bytes_ranks, ms_ranks, N, HBM_PEAK_GBS)
+    achieved = roof["achieved"]
+    f64 = None
+    if a.f64_leg:
+        if C is not None:
+            C.tile.free()
+            C = None
+        n_plans = len(plans)
+        f64 = f64_values_leg(cbg, grid, A, B, a, step, N)
+        del plans[n_plans:]  # the headline's phase plans only
 
     phases_run = plans[-1]["phases"] if plans else 1
     if rank == 0:
@@ -406,9 +491,15 @@ def main():
                                                  "before and 2 after the timed region",
                          "peak_measured_runs": peaks,
                          "traffic_source": traffic_src,
-                         "kernel": "local SpGEMM pipeline (symbolic+numeric), rank 0",
-                         "ms_avg": ms_avg, "bytes_alg": bytes_alg},
+                         "kernel": "local SpGEMM pipeline (symbolic+numeric) of every rank",
+                         "achieved_rule": "sum over ranks of bytes_alg / the slowest rank's device ms / N (per GPU)",
+                         "ms_avg": ms_ranks[roof["slowest_rank"]], "bytes_alg": sum(bytes_ranks),
+                         "ms_avg_ranks": [round(x, 3) for x in ms_ranks], "bytes_alg_ranks": bytes_ranks,
+                         "slowest_rank": roof["slowest_rank"], "slowest_rank_frac": roof["slowest_rank_frac"]},
         }
+        if f64 is not None:
+            out["roofline"]["frac_f64_values"] = f64["frac"]
+            out["f64_values"] = f64
         if N == 1 and not a.no_cpu_baseline:
             cores, host = host_cores()
             threads = a.cpu_threads or cores

@@ -35,7 +35,7 @@ namespace cbg {
 //   4: k_num_slab skips pass 1 products       8: k_num_slab skips the output writes
 __constant__ int c_dbg;
 //   16: k_num_slab accumulates per-phase wall time (thread 0 of every block) into g_phase
-__device__ unsigned long long g_phase[16];
+__device__ unsigned long long g_phase[24];
 //   32: k_num_slab counts into g_stat: slabs, non-full slabs, B entries, B entries of non-full slabs, products, nout
 //   64: k_sym_panel skips the hash-count products of sparse pairs and panel groups
 //  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
@@ -736,6 +736,7 @@ struct SymPanelArgs {
   int* gbm_next;
   int* gbm_slot;
   int gbm_min;
+  int pair_bm;  // count a sparse pair's rows in the panel bitmap (ds_or) instead of an LDS hash (CAS)
 };
 
 // staging of a unit fetched ahead: ok = 1: p0/p1 of the column; ok = 2: also
@@ -872,6 +873,40 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     phase_mark(tmark, 8);
     int T = 512;
     while (T * CBG_PAIR_LOAD_DEN < CBG_PAIR_LOAD_NUM * total) T <<= 1;
+    if (total <= SPARSE_SLAB_MAX && T <= pwords && a.pair_bm) {
+      // the count of a sparse pair from the panel bitmap: one ds_or per product
+      // (no returning CAS, no probes), a popcount of the panel's words; the
+      // zeroing is the hash table's for pairs of 2048-4096 products (32 KiB)
+      for (int j = tid; j < pwords / 4; j += BS) reinterpret_cast<uint4*>(bm)[j] = make_uint4(0u, 0u, 0u, 0u);
+      if (tid == 0) fine[0] = 0;
+      __syncthreads();
+      if (!(c_dbg & 64))
+        block_products<BS>(
+            pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
+            [&](const SegI& g, int u) { return irA[g.off + u] - R0; },
+            [&](int row) { atomicOr(&bm[row >> 5], 1u << (row & 31)); });
+      hook(2);
+      __syncthreads();
+      int count = 0;
+      for (int j = tid; j < words / 4 + 1; j += BS)
+        if (4 * j < words) {
+          const uint4 x = reinterpret_cast<const uint4*>(bm)[j];
+          count += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);  // (words past the panel's end are zero)
+        }
+      count = wave_sum(count);
+      if (lane_id() == 0 && count) atomicAdd(&fine[0], count);
+      __syncthreads();
+      if (tid == 0) {
+        const int cnt_pair = fine[0];
+        nslab[br] = cnt_pair ? 1 : 0;
+        if (cnt_pair) desc[(int64_t)br * NFINE_MAX] = make_int4(R0, R1, 0, cnt_pair | SLAB_SPARSE);
+        cnt_br[br] = cnt_pair;
+        if (gbm_slot) gbm_slot[br] = -1;
+        if (cnt_pair) atomicAdd(&cnt[col], cnt_pair);
+      }
+      phase_mark(tmark, 9);
+      return;
+    }
     if (total <= SPARSE_SLAB_MAX && T <= pwords) {
       if (c_dbg & 256) {
         __syncthreads();
@@ -1262,10 +1297,17 @@ struct __attribute__((aligned(16))) SlabRec {
 constexpr int SLAB_HASH_NCLS = 9;
 #define CBG_HASH_TABLES 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192
 __constant__ int c_hash_t[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
-constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS;
-__device__ __forceinline__ int slab_class(int w, int small_cap) {
+// + rank slabs (k_num_slab_rank) of <= 1024 / 2048 / 4096 nonzeros: the
+// hash-mode slabs of more than rank_min nonzeros spanning <= rank_span rows
+// (one panel; rank_span 0: none)
+constexpr int SLAB_RANK_NCLS = 3;
+constexpr int SLAB_RANK0 = 2 + SLAB_HASH_NCLS;
+constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS + SLAB_RANK_NCLS;
+__device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank_span, int rank_min) {
+  const int w = d.w;
   if (w & SLAB_SPARSE) {
     const int c = w & SLAB_CNT_MASK;
+    if (c > rank_min && d.y - d.x <= rank_span) return SLAB_RANK0 + (c <= 1024 ? 0 : c <= 2048 ? 1 : 2);
     int k = 0;
     while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
     return 2 + k;
@@ -1281,7 +1323,8 @@ __host__ __device__ inline int slab_kr(int R) { return SLAB_NCLS * R <= SLAB_KEY
 
 // pass 1: within-panel -> within-column offsets, (class, panel) counts
 __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
-                             int4* __restrict__ desc, int small_cap, int* __restrict__ counts) {
+                             int4* __restrict__ desc, int small_cap, int rank_span, int rank_min,
+                             int* __restrict__ counts) {
   extern __shared__ int lc[];  // [SLAB_NCLS * KR]
   const int KR = slab_kr(R), NK = SLAB_NCLS * KR;
   for (int k = threadIdx.x; k < NK; k += blockDim.x) lc[k] = 0;
@@ -1294,7 +1337,7 @@ __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab,
       for (int s = 0; s < nslab[br]; ++s) {
         int4& d = desc[(int64_t)br * NFINE_MAX + s];
         d.z += off;
-        atomicAdd(&lc[slab_class(d.w, small_cap) * KR + (KR > 1 ? r : 0)], 1);
+        atomicAdd(&lc[slab_class(d, small_cap, rank_span, rank_min) * KR + (KR > 1 ? r : 0)], 1);
       }
       off += cnt_br[br];
     }
@@ -1321,7 +1364,8 @@ __global__ void k_slab_bases(int R, const int* __restrict__ counts, int* __restr
 }
 // pass 2: slab records into their (class, panel) segment of one list
 __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, const int4* __restrict__ desc,
-                            int small_cap, int* __restrict__ cursor, SlabRec* __restrict__ list,
+                            int small_cap, int rank_span, int rank_min, int* __restrict__ cursor,
+                            SlabRec* __restrict__ list,
                             const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
                             const int64_t* __restrict__ colptr, const int* __restrict__ gbm_slot, int plog,
                             int64_t m_rows) {
@@ -1336,7 +1380,9 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
     for (int r = 0; r < R; ++r) {
       const int br = b * R + r;
       for (int s = 0; s < nslab[br]; ++s)
-        atomicAdd(&lc[slab_class(desc[(int64_t)br * NFINE_MAX + s].w, small_cap) * KR + (KR > 1 ? r : 0)], 1);
+        atomicAdd(&lc[slab_class(desc[(int64_t)br * NFINE_MAX + s], small_cap, rank_span, rank_min) * KR +
+                      (KR > 1 ? r : 0)],
+                  1);
     }
   __syncthreads();
   for (int k = threadIdx.x; k < NK; k += blockDim.x) {
@@ -1353,7 +1399,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
     const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
     for (int s = 0; s < nslab[br]; ++s) {
       const int4 d = desc[(int64_t)br * NFINE_MAX + s];
-      const int key = slab_class(d.w, small_cap) * KR + (KR > 1 ? r : 0);
+      const int key = slab_class(d, small_cap, rank_span, rank_min) * KR + (KR > 1 ? r : 0);
       SlabRec rec;
       rec.obase = cbase + d.z;
       rec.p0 = p0;
@@ -2193,6 +2239,106 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   }
 }
 
+// ----------------------------------------------------------------------------
+// per-product segment ids (hash and rank slabs)
+// ----------------------------------------------------------------------------
+// The flattened product loop (wave_products3) finds a product's segment (its
+// B entry) with a per-lane cursor that walks forward one segment per LDS read.
+// Where segments are short -- a (column, panel) pair reads A's columns inside
+// one row panel: 1-3 rows each at scale 22 -- a lane whose products lie 64
+// apart walks ~10 segments per product, a chain of dependent LDS reads before
+// each gather.  Instead the staging marks every nonempty segment's first
+// product (seg16[ex] = t) and a block max-scan spreads the marks, so each
+// product finds its segment with one LDS read and its (A offset, B value) with
+// a second: all of a thread's products issue their gathers back to back.
+struct __attribute__((aligned(16))) SegRec {
+  int off;  // A index of the segment's products minus the segment's first product index
+  int pad;
+  double b;  // the B entry's value
+};
+// inclusive max-scan over a wave of non-negative values (DPP, as wave_incl_scan)
+__device__ __forceinline__ int wave_incl_max(int v) {
+  v = max(v, dpp0<0x111>(v));
+  v = max(v, dpp0<0x112>(v));
+  v = max(v, dpp0<0x114>(v));
+  v = max(v, dpp0<0x118>(v));
+  v = max(v, dpp0<0x142, 0xa>(v));
+  v = max(v, dpp0<0x143, 0xc>(v));
+  return v;
+}
+// seg16[0, E*BS) zeroed, the heads written (seg16[ex] = t for every nonempty
+// segment t) and a barrier passed: spreads every head over its products (block
+// max-scan, thread t owns products E t .. E t + E - 1).  Ends with a barrier.
+template <int BS, int E>
+__device__ __forceinline__ void build_segids(unsigned short* seg16, int* tmp) {
+  constexpr int NW = BS / WAVE;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
+  int h[E];
+  if constexpr (E % 8 == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 8) {
+      const uint4 q = reinterpret_cast<const uint4*>(seg16 + tid * E + j)[0];
+      const unsigned v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        h[j + 2 * k] = (int)(v[k] & 0xffffu);
+        h[j + 2 * k + 1] = (int)(v[k] >> 16);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < E; ++j) h[j] = seg16[tid * E + j];
+  }
+  int m = 0;
+#pragma unroll
+  for (int j = 0; j < E; ++j) m = max(m, h[j]);
+  const int incl = wave_incl_max(m);
+  if (lane == WAVE - 1) tmp[w] = incl;
+  __syncthreads();
+  int before = 0;
+#pragma unroll
+  for (int v = 0; v < NW; ++v)
+    if (v < w) before = max(before, tmp[v]);
+  const int lprev = __shfl_up(incl, 1, WAVE);
+  int run = max(before, lane > 0 ? lprev : 0);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    run = max(run, h[j]);
+    h[j] = run;
+  }
+  if constexpr (E % 8 == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 8) {
+      unsigned v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = (unsigned)h[j + 2 * k] | ((unsigned)h[j + 2 * k + 1] << 16);
+      reinterpret_cast<uint4*>(seg16 + tid * E + j)[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < E; ++j) seg16[tid * E + j] = (unsigned short)h[j];
+  }
+  __syncthreads();
+}
+// products [0, total) by segment ids: thread t takes t + BS k (consecutive
+// threads, consecutive products: coalesced inside a segment), U in flight
+template <int BS, int U, class L, class A>
+__device__ __forceinline__ void block_products_sid(int total, const unsigned short* seg16, const SegRec* srec,
+                                                   L&& load, A&& apply) {
+  for (int u0 = threadIdx.x; u0 < total; u0 += U * BS) {
+    int sg[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) sg[j] = u0 + j * BS < total ? seg16[u0 + j * BS] : -1;
+    decltype(load(SegRec{}, 0)) x[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (sg[j] >= 0) x[j] = load(srec[sg[j]], u0 + j * BS);
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (sg[j] >= 0) apply(x[j]);
+  }
+}
+
 // numeric of a sparse (column, panel) pair (hash-mode slab, <= SPARSE_SLAB_MAX
 // products): LDS hash sized to the pair's nnz, sorted emit by row buckets
 #ifndef CBG_EMIT_MOFF  // emit ranks from cached in-bucket row offsets (1 LDS read per bucket member)
@@ -2216,11 +2362,12 @@ struct SlabHashLds {
   // vals[T] f64 | keys[T] | bv[BS] f64 | pref[BS+4] | st[BS] | tmp | boff[NB+4] | cur[NB] | members[MEMB] u16
   // bv|pref|st: idle during the emit, which reuses them for its in-bucket row
   // offsets (u16, MOFF) and, where both fit, its member list
-  static constexpr int IDLE = BS * 8 + (BS + 4) * 4 + BS * 4;
+  static constexpr int PBYTES = BS * 8 + (BS + 4) * 4 + BS * 4;  // staging region bv | pref | st
+  static constexpr int IDLE = PBYTES;
   static constexpr bool MOFF_FITS = MEMB * 2 <= IDLE;
   static constexpr bool MEMB_ALIAS = CBG_HASH_MEMB_ALIAS && 2 * MEMB * 2 <= IDLE;
-  static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
-                               (2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2);
+  static constexpr int TMP_OFF = T * 12 + PBYTES;
+  static constexpr int BYTES = TMP_OFF + (BS / WAVE + 4) * 4 + (2 * NB + 4) * 4 + (MEMB_ALIAS ? 0 : MEMB * 2);
 };
 
 #ifndef CBG_HASH_WPE  // waves per SIMD the hash-slab kernels are compiled for (0: the compiler's choice)
@@ -2256,7 +2403,7 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
   double* bv = reinterpret_cast<double*>(keys + T);  // T even: 8-B aligned
   int* pref = reinterpret_cast<int*>(bv + BS);
   int* st = pref + BS + 4;
-  int* tmp = st + BS;
+  int* tmp = reinterpret_cast<int*>(smem + L::TMP_OFF);
   int* boff = tmp + BS / WAVE + 4;
   int* cur = boff + NB + 4;
   unsigned short* members = L::MEMB_ALIAS ? reinterpret_cast<unsigned short*>(bv) + L::MEMB
@@ -2347,10 +2494,10 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
       if (c == nch - 1 && has_next) fetch1(nrec);
       if ((c_dbg & 32) && tid == 0) atomicAdd(&g_stat[CMLEN ? 8 : 7], (unsigned long long)total);
       if (!(c_dbg & 512))
-      block_products<BS>(
-          pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
-          [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
-          [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
+        block_products<BS>(
+            pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
+            [&](const SegV& g, int u) { return a_rowval<SR, VA>(irA, valA, g.off + u, g.b, 0); },
+            [&](const RowVal& x) { hash_acc_t<SR, T>(keys, vals, x.row, x.v); });
       __syncthreads();
       phase_mark(tmark, 14);
     }
@@ -2376,6 +2523,220 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
                                          rec.obase);
     __syncthreads();  // LDS is reset for the next slab
     phase_mark(tmark, 15);
+    if (!has_next) break;
+    i = inext;
+    rec = nrec;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// numeric of a hash-mode (column, panel) pair by bitmap rank: no hash, no sort
+// ----------------------------------------------------------------------------
+// A single-panel hash pair (<= SPARSE_SLAB_MAX products, one chunk of <=
+// BIG_BS B entries, rows inside one 2^plog panel).  The hash slab pays a
+// returning CAS chain per product and a bucket counting sort per entry; here:
+//   1. every lane gathers its <= RK products at once (all loads in flight) and
+//      keeps (row, value) in registers; it marks the rows in an LDS bitmap of
+//      the panel (ds_or, no return);
+//   2. a block scan of the popcounts of 4-word groups gives every group its
+//      first output rank (u16);
+//   3. each product's rank = group rank + popcount of the bits below it in its
+//      group; products accumulate at their ranks (vals[nout]);
+//   4. C's rows come straight out of the bitmap words, already in order
+//      (consecutive lanes own consecutive groups: the stores are consecutive
+//      positions), values copied from vals with coalesced stores.
+// The bitmap (32 KiB) is zeroed per slab and read twice in 16-byte vectors; every
+// random LDS access is one ds_or, two reads (group, its rank) and the semiring's
+// atomic per product.
+template <int NCAP, int BS>
+struct SlabRankLds {
+  // ust: during the products seg16[SPARSE_SLAB_MAX] u16 (each product's segment) |
+  //      srec[BS] (segment: A offset minus its first product index, B value);
+  //      from the rank scan on vals[NCAP] f64
+  // bm[SLAB_WORDS] | gpre[SLAB_WORDS / 4] u16 | tmp[BS/64+4]
+  static constexpr int SEG_BYTES = SPARSE_SLAB_MAX * 2;
+  static constexpr int UST = NCAP * 8 > SEG_BYTES + BS * 16 ? NCAP * 8 : SEG_BYTES + BS * 16;
+  static constexpr int BM_OFF = UST;
+  static constexpr int GPRE_OFF = BM_OFF + SLAB_WORDS * 4;
+  static constexpr int TMP_OFF = GPRE_OFF + (SLAB_WORDS / 4) * 2;
+  static constexpr int BYTES = TMP_OFF + (BS / WAVE + 4) * 4;
+  static_assert(SEG_BYTES % 16 == 0 && BM_OFF % 16 == 0 && GPRE_OFF % 16 == 0, "rank slab LDS alignment");
+};
+constexpr int RANK_BS = 512;
+static_assert(SPARSE_SLAB_MAX % RANK_BS == 0 && SPARSE_SLAB_MAX / RANK_BS <= 16, "rank slab products per lane");
+static_assert(SPARSE_SLAB_MAX == 8 * RANK_BS, "segment scan: 8 products per thread");
+
+__device__ __forceinline__ int popc4(const uint4& q) {
+  return __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
+}
+template <int SR, int NCAP, int BS, typename VA>
+__global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict__ list, int n,
+                                                      int* __restrict__ queue, const int32_t* __restrict__ irB,
+                                                      const double* __restrict__ valB,
+                                                      const int2* __restrict__ cmapP, int64_t nA1,
+                                                      const int32_t* __restrict__ irA, const VA* __restrict__ valA,
+                                                      int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
+  using L = SlabRankLds<NCAP, BS>;
+  constexpr int NW = BS / WAVE;
+  constexpr int RK = SPARSE_SLAB_MAX / BS;  // products per thread
+  constexpr int NG = SLAB_WORDS / 4;        // 4-word groups of a panel
+  constexpr int GPT = NG / BS;              // groups per thread in the rank scan
+  static_assert(GPT == 4, "rank scan packs 4 u16 group ranks per thread");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* vals = reinterpret_cast<double*>(smem);
+  unsigned short* seg16 = reinterpret_cast<unsigned short*>(smem);
+  SegRec* srec = reinterpret_cast<SegRec*>(smem + L::SEG_BYTES);
+  unsigned* bm = reinterpret_cast<unsigned*>(smem + L::BM_OFF);
+  uint4* bm4 = reinterpret_cast<uint4*>(smem + L::BM_OFF);
+  unsigned short* gpre = reinterpret_cast<unsigned short*>(smem + L::GPRE_OFF);
+  int* tmp = reinterpret_cast<int*>(smem + L::TMP_OFF);
+  const int tid = threadIdx.x, lane = lane_id(), w = tid / WAVE;
+  int i = blockIdx.x;
+  if (i >= n) return;
+  // next slab's staging (one B entry per thread), fetched while this one runs
+  int p_ir = 0;
+  double p_bv = 0.0;
+  int2 p_ce = make_int2(0, 0);
+  auto fetch1 = [&](const SlabRec& r) {
+    if (tid < r.nb) {
+      p_ir = irB[r.p0 + tid];
+      p_bv = valB[r.p0 + tid];
+    }
+  };
+  auto fetch2 = [&](const SlabRec& r) {
+    if (tid < r.nb) p_ce = cmapP[(int64_t)r.r * nA1 + p_ir];
+  };
+  SlabRec rec = list[i];
+  fetch1(rec);
+  fetch2(rec);
+  while (true) {
+    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    unsigned long long tmark = wall_clock64();
+    const int lo = rec.lo, nout = rec.nout;
+    const int ng = (((rec.hi - lo + 31) >> 5) + 3) >> 2;
+    const int64_t obase = rec.obase;
+    for (int g = tid; g < ng; g += BS) bm4[g] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(seg16)[tid] = make_uint4(0u, 0u, 0u, 0u);  // 8 products per thread
+    // staging: segment t = B entry t; its first product at ex; heads of the
+    // nonempty segments marked at their first product
+    const int len = tid < rec.nb ? p_ce.y - p_ce.x : 0;
+    int total;
+    const int ex = block_excl_scan<BS>(len, tmp, &total);  // (its barriers order the zeroing above)
+    srec[tid] = SegRec{(tid < rec.nb ? p_ce.x : 0) - ex, 0, tid < rec.nb ? p_bv : 0.0};
+    if (len > 0) seg16[ex] = (unsigned short)tid;
+    const int inext = tmp[NW + 2];
+    const bool has_next = inext < n;
+    SlabRec nrec;
+    if (has_next) nrec = list[inext];
+    __syncthreads();
+    build_segids<BS, RK>(seg16, tmp);  // every product's segment
+    phase_mark(tmark, 16);
+    // 1. products into registers (thread t: t + BS k), rows marked in the bitmap
+    int xr[RK];
+    double xv[RK];
+    {
+      int sg[RK];
+#pragma unroll
+      for (int k = 0; k < RK; ++k) {
+        const int u = tid + k * BS;
+        sg[k] = u < total ? seg16[u] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < RK; ++k) {
+        xr[k] = -1;
+        if (sg[k] >= 0 && !(c_dbg & 512)) {
+          const SegRec r = srec[sg[k]];
+          const RowVal x = a_rowval<SR, VA>(irA, valA, r.off + tid + k * BS, r.b, lo);
+          xr[k] = x.row;
+          xv[k] = x.v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < RK; ++k)
+        if (xr[k] >= 0) atomicOr(&bm[xr[k] >> 5], 1u << (xr[k] & 31));
+    }
+    if (has_next) fetch1(nrec);
+    __syncthreads();
+    phase_mark(tmark, 17);
+    // 2. group ranks: thread t owns groups 4t .. 4t+3 (one 8-byte store of 4
+    // u16); vals (aliasing the staging, now idle) set to the semiring's identity
+    {
+      const double id = Sem<SR>::identity();
+      double2* v2 = reinterpret_cast<double2*>(vals);
+      for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
+      uint4 q[GPT];
+      int sum = 0;
+#pragma unroll
+      for (int j = 0; j < GPT; ++j) {
+        const int g = tid * GPT + j;
+        q[j] = g < ng ? bm4[g] : make_uint4(0u, 0u, 0u, 0u);
+        sum += popc4(q[j]);
+      }
+      int tot;
+      int run = block_excl_scan<BS>(sum, tmp, &tot);
+      unsigned pk[GPT / 2];
+#pragma unroll
+      for (int j = 0; j < GPT; j += 2) {
+        const unsigned a = (unsigned)run;
+        run += popc4(q[j]);
+        pk[j / 2] = a | ((unsigned)run << 16);
+        run += popc4(q[j + 1]);
+      }
+      *reinterpret_cast<uint2*>(gpre + tid * GPT) = make_uint2(pk[0], pk[1]);
+    }
+    __syncthreads();
+    phase_mark(tmark, 18);
+    // 3. accumulate at the ranks (all lookups first, then the atomics)
+    {
+      int rk[RK];
+#pragma unroll
+      for (int k = 0; k < RK; ++k) {
+        rk[k] = -1;
+        if (xr[k] >= 0) {
+          const int r = xr[k], wd = r >> 5, g = wd >> 2, j = wd & 3;
+          const uint4 q = bm4[g];
+          const unsigned below = (1u << (r & 31)) - 1u;
+          int x = gpre[g];
+          x += j > 0 ? __popc(q.x) : __popc(q.x & below);
+          if (j >= 1) x += j > 1 ? __popc(q.y) : __popc(q.y & below);
+          if (j >= 2) x += j > 2 ? __popc(q.z) : __popc(q.z & below);
+          if (j >= 3) x += __popc(q.w & below);
+          rk[k] = x;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < RK; ++k)
+        if (rk[k] >= 0) Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
+    }
+    if (has_next) fetch2(nrec);
+    __syncthreads();
+    phase_mark(tmark, 19);
+    // 4. rows from the bitmap (sorted), values from vals
+    if (!(c_dbg & 1024)) {
+      for (int g = tid; g < ng; g += BS) {
+        const uint4 q = bm4[g];
+        if (q.x | q.y | q.z | q.w) {
+          int pos = gpre[g];
+          const unsigned wv[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            unsigned x = wv[j];
+            const int rb = lo + ((g * 4 + j) << 5) - 1;
+            while (x) {
+              out_ir[obase + pos++] = rb + __ffs(x);
+              x &= x - 1;
+            }
+          }
+        }
+      }
+      for (int j = tid; j < nout; j += BS) st_emit(&out_val[obase + j], vals[j]);
+    }
+    if ((c_dbg & 32) && tid == 0) {
+      atomicAdd(&g_stat[10], (unsigned long long)total);
+      atomicAdd(&g_stat[11], (unsigned long long)nout);
+    }
+    __syncthreads();  // LDS is reset for the next slab
+    phase_mark(tmark, 20);
     if (!has_next) break;
     i = inext;
     rec = nrec;
@@ -2664,6 +3025,37 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   df.take(queue);
 }
 
+template <int SR, int NCAP>
+static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
+                             cbg_tile& C, hipStream_t s, DeferredFree& df) {
+  if (n <= 0) return;
+  constexpr int L = SlabRankLds<NCAP, RANK_BS>::BYTES;
+  DBuf<int> queue(1);
+  CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
+  auto go = [&](auto k, const auto* valA, int& per_cu) {
+    set_lds(k, L);
+    if (!per_cu) {
+      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, RANK_BS, L));
+      if (per_cu < 1) per_cu = 1;
+    }
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, B.ir, B.val, bp.cmapP,
+                       A.n + 1, A.ir, valA, C.ir, C.val);
+  };
+  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
+  if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV>, bp.valAp, per_cu_p);
+  else if (bp.valAf) go(k_num_slab_rank<SR, NCAP, RANK_BS, float>, bp.valAf, per_cu_f);
+  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double>, A.val, per_cu_d);
+  df.take(queue);
+}
+
+// hash-mode single-panel slabs of more than this many nonzeros run as rank
+// slabs (CBG_RANK_MIN overrides; < 0: none)
+static int rank_slabs_min() {
+  static const char* e = getenv("CBG_RANK_MIN");
+  return e ? atoi(e) : 683;
+}
+
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 // bit c: hash slab class c (CBG_HASH_TABLES order) runs on the side stream
 // (CBG_SIDE_HASH overrides)
@@ -2694,14 +3086,13 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_hash<SR, 1024, 256>(at[4], ncls[4], bp, A, B, C, hs(2), df);
   launch_slab_hash<SR, 1536, 256>(at[5], ncls[5], bp, A, B, C, hs(3), df);
   launch_slab_hash<SR, 2048, 256>(at[6], ncls[6], bp, A, B, C, hs(4), df);
-#ifndef CBG_HBS_3072
-#define CBG_HBS_3072 512
-#define CBG_HBS_4096 512
-#endif
-  launch_slab_hash<SR, 3072, CBG_HBS_3072>(at[7], ncls[7], bp, A, B, C, hs(5), df);
-  launch_slab_hash<SR, 4096, CBG_HBS_4096>(at[8], ncls[8], bp, A, B, C, hs(6), df);
+  launch_slab_hash<SR, 3072, 512>(at[7], ncls[7], bp, A, B, C, hs(5), df);
+  launch_slab_hash<SR, 4096, 512>(at[8], ncls[8], bp, A, B, C, hs(6), df);
   launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, hs(7), df);
   launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, hs(8), df);
+  launch_slab_rank<SR, 4096>(at[SLAB_RANK0 + 2], ncls[SLAB_RANK0 + 2], bp, A, B, C, s, df);
+  launch_slab_rank<SR, 2048>(at[SLAB_RANK0 + 1], ncls[SLAB_RANK0 + 1], bp, A, B, C, s, df);
+  launch_slab_rank<SR, 1024>(at[SLAB_RANK0], ncls[SLAB_RANK0], bp, A, B, C, s, df);
 
 }
 
@@ -2710,6 +3101,13 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
 static int gbm_min_products() {
   static const char* e = getenv("CBG_GBM_MIN");
   return e ? atoi(e) : 0;
+}
+
+// sparse (column, panel) pairs counted in the panel bitmap (CBG_SYM_PAIR_BM=0:
+// by the LDS hash, before round 5)
+static int sym_pair_bitmap() {
+  static const char* e = getenv("CBG_SYM_PAIR_BM");
+  return e && !strcmp(e, "1");
 }
 
 // kept symbolic bitmaps (32 KiB per (column, panel) pair): CBG_BITMAP_BUDGET_GB,
@@ -3314,7 +3712,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
-                    bp.gbm_slot.p, gbm_min_products()};
+                    bp.gbm_slot.p, gbm_min_products(), sym_pair_bitmap()};
     // one launch per group class (largest groups first)
     for (int c = 0; c < NGCLS; ++c) {
       const int nc = sb.count[NSMALL + c];
@@ -3434,12 +3832,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const int NK = SLAB_NCLS * slab_kr(bp.R);
     DBuf<int> counters(2 * NK + SLAB_NCLS);  // counts[NK] | cursor[NK] | class totals
     CBG_HIP(hipMemsetAsync(counters.p, 0, (2 * NK + SLAB_NCLS) * sizeof(int), s));
+    const int rank_span = rank_slabs_min() >= 0 ? 1 << bp.plog : 0, rank_min = rank_slabs_min();
     hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), NK * sizeof(int), s, nbig, bp.R, bp.nslab.p,
-                       bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, counters.p);
+                       bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p);
     hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, bp.R, counters.p, counters.p + NK,
                        counters.p + 2 * NK);
     hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 2 * NK * sizeof(int), s, nbig, bp.R,
-                       bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, counters.p + NK, slist.p, bp.perm_big, B.cp, colptr.p,
+                       bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p + NK, slist.p,
+                       bp.perm_big, B.cp, colptr.p,
                        bp.gbm_slot.p, bp.plog, A.m);
     int* ncls_h = reinterpret_cast<int*>(host_stage(STAGE_SLABS));
     CBG_HIP(hipMemcpyAsync(ncls_h, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -3452,6 +3852,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       static const int ht[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
       std::fprintf(stderr, "[cbg slabs] bitmap small %d large %d | hash", ncls[0], ncls[1]);
       for (int k = 0; k < SLAB_HASH_NCLS; ++k) std::fprintf(stderr, " T%d %d", ht[k], ncls[2 + k]);
+      std::fprintf(stderr, " | rank N1024 %d N2048 %d N4096 %d", ncls[SLAB_RANK0], ncls[SLAB_RANK0 + 1],
+                   ncls[SLAB_RANK0 + 2]);
       std::fprintf(stderr, "\n");
     }
   }
@@ -3528,12 +3930,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
         unsigned long long gs[12];
         CBG_HIP(hipMemcpyFromSymbol(gs, HIP_SYMBOL(g_stat), sizeof(gs)));
         std::fprintf(stderr, "[cbg k_num_slab] slabs %llu nonfull %llu nb %llu nb_nonfull %llu nout %llu multichunk %llu "
-                     "products %llu | hash products panel %llu column %llu nout %llu\n",
-                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6], gs[4], gs[7], gs[8], gs[9]);
+                     "products %llu | hash products panel %llu column %llu nout %llu | rank products %llu nout %llu\n",
+                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6], gs[4], gs[7], gs[8], gs[9], gs[10], gs[11]);
         std::memset(gs, 0, sizeof(gs));
         CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stat), gs, sizeof(gs)));
       }
-      unsigned long long ph[16];
+      unsigned long long ph[24];
       CBG_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph)));
       const char* names[7] = {"init", "staging", "-", "rankscan", "pass0", "pass1", "output"};
       std::fprintf(stderr, "[cbg phases, block-us summed / 256 CUs]");
@@ -3544,6 +3946,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       const char* hnames[4] = {"hash_clear", "hash_staging", "hash_products", "hash_emit"};
       const int hk[4] = {7, 13, 14, 15};
       for (int k = 0; k < 4; ++k) std::fprintf(stderr, " %s=%.3fms", hnames[k], ph[hk[k]] / 100.0 / 256.0 / 1000.0);
+      const char* rnames[5] = {"rank_stage", "rank_products", "rank_scan", "rank_acc", "rank_emit"};
+      for (int k = 0; k < 5; ++k) std::fprintf(stderr, " %s=%.3fms", rnames[k], ph[16 + k] / 100.0 / 256.0 / 1000.0);
       std::fprintf(stderr, "\n");
       std::memset(ph, 0, sizeof(ph));
       CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phase), ph, sizeof(ph)));

@@ -14,10 +14,11 @@
 #pragma once
 #include <mpi.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <limits>
 #include <map>
-#include <tuple>
 #include <vector>
 
 #include "CombBLAS/CombBLAS.h"
@@ -51,19 +52,52 @@ static cbg_tile cbg_upload(const SpDCCols<IT, double>& T) {
   return dev;
 }
 
-// device tile -> SpDCCols (the tuples constructor, SpDCCols.cpp:197)
+// largest value IT may hold here: numeric_limits<IT>::max(), or the test hook
+// CBG_ADAPTER_IT_MAX when that is smaller (tests force the overflow path)
+template <class IT>
+static int64_t cbg_index_limit() {
+  int64_t lim = (int64_t)std::numeric_limits<IT>::max();
+  if (const char* e = std::getenv("CBG_ADAPTER_IT_MAX")) lim = std::min<int64_t>(lim, std::atoll(e));
+  return lim;
+}
+
+// device tile -> SpDCCols with no host tuples: SpDCCols(size, nRow, nCol, nzc)
+// (SpDCCols.cpp:55-62) allocates the Dcsc of exactly nnz entries and nzc
+// columns (Dcsc(nnz, nzcol), dcsc.cpp:44-52: cp/jc/ir/numx, dcsc.h:124-131),
+// and the download writes C's arrays into it: the values straight into numx,
+// the indices straight where their width is IT's (int32 ir/jc for IT = int,
+// int64 cp for IT = int64_t), through one staging copy otherwise.  A C whose
+// nnz or dimensions IT cannot represent aborts with a message (the tuples
+// constructor's (IT)t.size() wrapped silently).
 template <class IT>
 static SpDCCols<IT, double>* cbg_download(const cbg_tile& C) {
-  std::vector<int64_t> cp(C.nzc + 1);
-  std::vector<int32_t> jc(C.nzc), ir(C.nnz);
-  std::vector<double> v(C.nnz);
-  cbg_tile h{0, 0, 0, 0, cp.data(), jc.data(), ir.data(), v.data(), 0, 0};
+  const int64_t lim = cbg_index_limit<IT>();
+  if (C.nnz > lim || C.m > lim || C.n > lim) {
+    std::fprintf(stderr,
+                 "[cbg adapter] C of %lld x %lld with %lld nonzeros exceeds the index type's range (%lld): "
+                 "use SpDCCols<int64_t, double>\n",
+                 (long long)C.m, (long long)C.n, (long long)C.nnz, (long long)lim);
+    MPI_Abort(MPI_COMM_WORLD, CBG_ERR_NOTSUPPORTED);
+  }
+  if (C.nnz == 0) return new SpDCCols<IT, double>(0, (IT)C.m, (IT)C.n, 0);
+  SpDCCols<IT, double>* T = new SpDCCols<IT, double>((IT)C.nnz, (IT)C.m, (IT)C.n, (IT)C.nzc);
+  Dcsc<IT, double>* d = T->GetDCSC();
+  constexpr bool narrow = sizeof(IT) == sizeof(int32_t);
+  std::vector<int64_t> cp64(narrow ? C.nzc + 1 : 0);
+  std::vector<int32_t> jc32(narrow ? 0 : C.nzc), ir32(narrow ? 0 : C.nnz);
+  cbg_tile h{0, 0, 0, 0,
+             narrow ? cp64.data() : reinterpret_cast<int64_t*>(d->cp),
+             narrow ? reinterpret_cast<int32_t*>(d->jc) : jc32.data(),
+             narrow ? reinterpret_cast<int32_t*>(d->ir) : ir32.data(),
+             d->numx, 0, 0};
   if (int rc = cbg_tile_download(&C, &h)) MPI_Abort(MPI_COMM_WORLD, rc);
-  std::vector<std::tuple<IT, IT, double>> t;
-  t.reserve(C.nnz);
-  for (int64_t i = 0; i < C.nzc; ++i)
-    for (int64_t p = cp[i]; p < cp[i + 1]; ++p) t.emplace_back((IT)ir[p], (IT)jc[i], v[p]);
-  return new SpDCCols<IT, double>((IT)C.m, (IT)C.n, (IT)t.size(), t.data(), false);
+  if (narrow) {
+    for (int64_t i = 0; i <= C.nzc; ++i) d->cp[i] = (IT)cp64[i];
+  } else {
+    for (int64_t i = 0; i < C.nzc; ++i) d->jc[i] = (IT)jc32[i];
+    for (int64_t p = 0; p < C.nnz; ++p) d->ir[p] = (IT)ir32[p];
+  }
+  return T;
 }
 
 // one RCCL grid per CommGrid, created collectively from its world communicator

@@ -1175,6 +1175,46 @@ def test_random_values_scale24_piece_vs_oracle(cbg):
     assert_tiles_equal(Ch, ref, rtol=RTOL, bound=bound)
 
 
+S22_VALUE_PIECES = (0, 37, 101, 166, 230, 295, 359, 424, 480, 511)
+
+
+def test_random_values_scale22_pieces_vs_oracle(cbg):
+    """The f64-value path at the headline's own shape: the
+    scale-22 R-MAT tile (R = 16 row panels) with values U[-1, 1) from a hash of (row,
+    col) -- A's values are then f64, so the slab kernels' f64 instantiations run, not
+    the f32 narrowing of R-MAT's integer values -- times B-column pieces of 1/512 of
+    the tile (B = A's columns [p n/512, (p+1) n/512)) for 10 pieces spread over the
+    columns, the high-id end included.  Every piece has big columns over 16 panels:
+    bitmap pairs (single- and multi-slab), rank slabs (single-panel sparse pairs),
+    hash slabs (panel groups).  Entry by entry against the CPU oracle: plus-times
+    within 1e-12 (|A||B|)_ij; min-plus exact on three of the pieces
+    (mtSpGEMM.h:362-440 semantics, Dcsc::operator== dcsc.cpp:472-510)."""
+    n = 1 << 22
+    A = cbg.rmat_tile(22, 16).set_random_values()
+    Ah = A.to_host()
+    for p in S22_VALUE_PIECES:
+        c0, c1 = p * (n // 512), (p + 1) * (n // 512)
+        left, right = A.split_cols(c1)
+        right.free()
+        low, B = left.split_cols(c0)
+        low.free()
+        left.free()
+        Bh = B.to_host()  # columns renumbered from 0, as C's
+        for sr in (("plus", "minplus") if p in (0, 230, 511) else ("plus",)):
+            C = cbg.LocalHybridSpGEMM(A, B, sr)
+            st = cbg.last_stats()
+            assert st["n_big"] > 0 and st["n_slabs"] > 0, (p, st)
+            Ch = C.to_host()
+            C.free()
+            ref = oracle_local(Ah, Bh, sr)
+            if sr == "plus":
+                assert_tiles_equal(Ch, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+            else:
+                assert_tiles_equal(Ch, ref)
+        B.free()
+    A.free()
+
+
 def test_local_scale24_column_pieces_vs_oracle(cbg):
     """Scale 24 (2^24 rows: R = 64 row panels, groups of up to 64 panels) pinned
     against the CPU oracle on a sample of C: column pieces p of 512 (B = A's
@@ -1313,6 +1353,24 @@ def test_reference_multtiming_unmodified_dropin():
     assert "[cbg adapter] Mult_AnXBn_DoubleBuff on MI355X" in out and "[cbg adapter] Mult_AnXBn_Synch on MI355X" in out
     assert "Double buffered multiplications finished" in out and "Synchronous multiplications finished" in out
     assert "29677" in out  # C's nonzeros, printed by the reference's SpParHelper::Print / PrintInfo
+
+
+def test_reference_dropin_index_overflow():
+    """The drop-in's download (integration/ParFriends_cbg.h cbg_download) fills the
+    reference's Dcsc arrays directly and refuses a C whose nonzeros the index type
+    cannot hold (the tuples constructor's (IT)t.size() wrapped silently): with the
+    limit forced to 1000 (CBG_ADAPTER_IT_MAX) the unmodified MultTiming aborts with
+    the message instead of building a wrong matrix (largeseq: 29,677 nonzeros)."""
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    os.environ["CBG_ADAPTER_IT_MAX"] = "1000"
+    try:
+        rc, out = _run_tool(("oracle", "_ref", "multtiming_dropin"),
+                            [os.path.join(gold, "largeseq_input1_0.triples"), os.path.join(gold, "largeseq_input2_0.triples")])
+    finally:
+        del os.environ["CBG_ADAPTER_IT_MAX"]
+    assert rc != 0, out[-2000:]
+    assert "exceeds the index type's range (1000)" in out and "29677 nonzeros" in out, out[-2000:]
 
 
 def test_tile_plugin_surface_python(cbg):

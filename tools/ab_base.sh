@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the committed HEAD (or a given rev) of libcbg into build/variants/base for same-box A/B sweeps:
-#   tools/ab_base.sh [rev]  then  tools/sweep.sh out default base
+#   tools/ab_base.sh [rev]  then  VARIANTS="tree base" tools/gpu_libab.sh (on the GPU box)
 set -e
 rev=${1:-HEAD}
 root=$(cd "$(dirname "$0")/.." && pwd)
