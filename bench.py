@@ -465,7 +465,8 @@ def main():
                                if plans else None),
                 "double_buffering": {"pieces": [p_["pieces"] for p_ in pipe],
                                      "decision": [["one piece", "pipelined", "adaptive: pipelined",
-                                                   "adaptive: rejoined"][p_["rule"]] for p_ in pipe],
+                                                   "adaptive: rejoined", "fixed pipeline"][p_["rule"]]
+                                                  if p_["pieces"] > 1 or p_["rule"] else "one piece" for p_ in pipe],
                                      "bytes_bcast_rank0": [p_["bytes_recv"] for p_ in pipe],
                                      "exposed_comm_ms": [round(p_["exposed_comm_ms"], 3) for p_ in pipe],
                                      "bcast_ms_piece0": [round(p_["bcast_ms_piece0"], 3) for p_ in pipe],

@@ -223,13 +223,17 @@ void thin_copy(const int32_t* perm, int n, const int64_t* tslot, const int32_t* 
 
 // radix sort of (key, value) pairs (cbg_sort.hip): LSD over the 8-bit digits
 // that `varying` marks as possibly nonzero, stable, 64-bit counts; the sorted
-// pairs end in `keys` / `vals` (the DBufs may be swapped with temporaries)
+// pairs end in `keys` / `vals` (the DBufs may be swapped with temporaries).
+// With df the temporaries are handed to it (no host synchronization: the
+// caller's stream sync releases them), else the call synchronizes the stream.
 template <typename K>
-void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned long long varying, hipStream_t s);
-// equal consecutive keys combined with the semiring's add (in order); returns the runs
+void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned long long varying, hipStream_t s,
+                      DeferredFree* df = nullptr);
+// equal consecutive keys combined with the semiring's add (in order); returns the
+// runs (one readback: a host synchronization; temporaries to df when given)
 template <typename K>
 int64_t reduce_by_key(const K* keys, const double* vals, int64_t n, int semiring, K* ukeys, double* uvals,
-                      hipStream_t s);
+                      hipStream_t s, DeferredFree* df = nullptr);
 
 // multiway merge of column-sorted partial tiles (cbg_merge.hip)
 // int64 entry counts: column chunks of < 2^30 stacked entries (CBG_MERGE_CHUNK

@@ -7,7 +7,7 @@
 //
 // Pipeline (all on one HIP stream):
 //   k_colmap      dense column map of A            (Dcsc::ConstructAux/FillColInds, dcsc.cpp:982-1343)
-//   k_flops       flops per B column               (estimateFLOP, mtSpGEMM.h:1056-1134)
+//   k_flops_seg   flops per B column               (estimateFLOP, mtSpGEMM.h:1056-1134)
 //   classify/bin  columns binned by flops
 //   k_sym_*       exact nnz per C column            (estimateNNZ_Hash, mtSpGEMM.h:805-933)
 //                 wave-level LDS hash (F<=512), block LDS hash (F<=4096),
@@ -22,6 +22,7 @@
 // staged in LDS with a prefix sum of A-column lengths, and consecutive lanes
 // take consecutive products, so reads of A's columns are coalesced whatever
 // their length (R-MAT hub columns included).
+#include <atomic>
 #include <cstring>
 #include <type_traits>
 
@@ -92,65 +93,6 @@ __global__ void k_inline_cols(int64_t n1, const int2* __restrict__ cmap, const i
   ainl[2 * k + 1] = v;
 }
 
-// flops of every B column: FLOP_G lanes per column (B columns are short on
-// average; a whole wave per column would leave most lanes idle).  A group
-// sums at most FLOP_HEAD entries of its column and queues a longer column
-// (R-MAT hubs: 10^4-10^5 entries, whose serial tail would set the kernel's
-// time) for k_flops_tail, where a whole block sums the rest.
-#ifndef CBG_FLOP_G  // scale 22, per phase: 8/512 0.52 ms, 16/512 0.76, 8/256 0.59, 4/512 0.57, 8/1024 0.54
-#define CBG_FLOP_G 8
-#define CBG_FLOP_HEAD 512
-#endif
-constexpr int FLOP_G = CBG_FLOP_G;
-constexpr int FLOP_HEAD = CBG_FLOP_HEAD;
-// flops[nzcB] accumulates the total (one atomic per block)
-__global__ void k_flops(int64_t nzcB, const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                        const int2* __restrict__ cmap, int64_t* __restrict__ flops, int* __restrict__ longq) {
-  __shared__ unsigned long long bsum;
-  if (threadIdx.x == 0) bsum = 0;
-  __syncthreads();
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t w = t / FLOP_G;
-  const int g = (int)(t % FLOP_G);
-  long long s = 0;
-  if (w < nzcB) {
-    const int64_t p0 = cpB[w], p1 = cpB[w + 1];
-    const int64_t pe = p1 - p0 > FLOP_HEAD ? p0 + FLOP_HEAD : p1;
-    for (int64_t p = p0 + g; p < pe; p += FLOP_G) s += cmap[irB[p]].y;
-    if (g == 0 && pe < p1) longq[1 + atomicAdd(&longq[0], 1)] = (int)w;
-  }
-#pragma unroll
-  for (int d = FLOP_G / 2; d > 0; d >>= 1) s += __shfl_xor(s, d, FLOP_G);
-  if (w < nzcB && g == 0) {
-    flops[w] = s;
-    atomicAdd(&bsum, (unsigned long long)s);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && bsum) atomicAdd(reinterpret_cast<unsigned long long*>(flops + nzcB), bsum);
-}
-// the entries past FLOP_HEAD of the queued columns: a block per column
-// (grid-stride over the queue, whose length only the device knows)
-__global__ __launch_bounds__(256) void k_flops_tail(const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
-                                                    const int2* __restrict__ cmap, int64_t nzcB,
-                                                    int64_t* __restrict__ flops, const int* __restrict__ longq) {
-  __shared__ long long part[256 / WAVE];
-  const int nq = longq[0];
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-    const int w = longq[1 + q];
-    long long s = 0;
-    for (int64_t p = cpB[w] + FLOP_HEAD + threadIdx.x; p < cpB[w + 1]; p += blockDim.x) s += cmap[irB[p]].y;
-    for (int d = WAVE / 2; d > 0; d >>= 1) s += __shfl_xor(s, d);
-    if (lane_id() == 0) part[threadIdx.x / WAVE] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      long long tot = 0;
-      for (int k = 0; k < 256 / WAVE; ++k) tot += part[k];
-      flops[w] += tot;  // this block owns column w's entry (k_flops wrote its head)
-      atomicAdd(reinterpret_cast<unsigned long long*>(flops + nzcB), (unsigned long long)tot);
-    }
-    __syncthreads();
-  }
-}
 
 // flops of every B column, load-balanced over B's ENTRIES (merge-path style):
 // block b takes entries [b*E, (b+1)*E), finds the column holding its first
@@ -737,6 +679,12 @@ struct SymPanelArgs {
   int* gbm_slot;
   int gbm_min;
   int pair_bm;  // count a sparse pair's rows in the panel bitmap (ds_or) instead of an LDS hash (CAS)
+  // a multi-slab pair's cut positions (offsets into each B entry's run at every
+  // inner slab boundary) for the numeric: cuts[pcoff[br] + (s - 1) * nb + j]
+  int* cuts;
+  unsigned long long* cuts_next;
+  long long cuts_cap;
+  int* pcoff;  // per (column, panel) pair, -1: none (pre-set)
 };
 
 // staging of a unit fetched ahead: ok = 1: p0/p1 of the column; ok = 2: also
@@ -761,6 +709,7 @@ struct SymPanelLds {
 // rows of the symbolic overflow list: what is left of 160 KiB / 4 blocks per
 // CU after the 8192-word bitmap and the staging arrays (the launch keeps 4 blocks)
 constexpr int SYM_OVF_CAP = CBG_SYM_OVF > 0 ? 896 : 0;
+static_assert(SYM_OVF_CAP >= NFINE_MAX + 2, "the cut pass keeps a pair's slab rows in the overflow list");
 
 // hash_claim with at most NPROBE probes; a row without a slot by then goes to
 // an LDS overflow list (one atomic per wave) that dense waves insert after the
@@ -1074,6 +1023,39 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       cnt_br[br] = total;
       nslab[br] = ns;
       if (total) atomicAdd(&cnt[col], total);
+      // for the cut pass: the slab count and the slabs' first rows (in the
+      // overflow list, idle on the bitmap path)
+      for (int q = 1; q < ns; ++q) L.ovf[1 + q] = d[q].x;
+      L.ovf[0] = ns;
+    }
+  }
+  if (a.cuts) {
+    // Cut positions of a multi-slab pair, once: for every B entry the start of
+    // its A run's part in each slab after the first (a lower bound per slab
+    // boundary, the run's rows ascending), as offsets from the run's start.
+    // The numeric staged two binary searches per entry per slab instead.
+    __syncthreads();
+    const int ns = L.ovf[0];
+    if (ns > 1) {
+      const int64_t nb = p1 - p0;
+      if (tid == 0) {
+        const long long need = (long long)(ns - 1) * nb;
+        long long off = (long long)atomicAdd(a.cuts_next, (unsigned long long)need);
+        if (off + need > a.cuts_cap) off = -1;
+        a.pcoff[br] = (int)off;
+        L.ovf[1] = (int)off;
+      }
+      __syncthreads();
+      const int off = L.ovf[1];
+      if (off >= 0)
+        for (int64_t j = tid; j < nb; j += BS) {
+          const int2 ce = cm[irB[p0 + j]];
+          int pos = ce.x;
+          for (int q = 1; q < ns; ++q) {
+            pos = lower_bound_g(irA, pos, ce.y, L.ovf[1 + q]);
+            a.cuts[(int64_t)off + (int64_t)(q - 1) * nb + j] = pos - ce.x;
+          }
+        }
     }
   }
   if (c_dbg & 16) {
@@ -1282,9 +1264,13 @@ struct __attribute__((aligned(16))) SlabRec {
   int lo, hi;     // row range
   int nout;       // nnz of the slab
   int slot;       // kept symbolic bitmap (-1: none)
-  int full;       // A's whole panel runs are the slab's products (the slab is its panel, or its pair's only slab)
-  int ends;       // bit 0: first slab of its (column, panel) pair, bit 1: last
+  // bit 0: first slab of its (column, panel) pair, bit 1: last, bit 2 (SLAB_FULL):
+  // A's whole panel runs are the slab's products (the slab is its panel, or its
+  // pair's only slab); bits 3+: the slab's index in its pair
+  int flags;
+  int coff;       // the pair's precomputed cut offsets in `cuts` (-1: search them)
 };
+constexpr int SLAB_FULL = 4;
 
 #ifndef CBG_HASH_LOAD_NUM  // numeric hash slab tables: T >= (NUM/DEN) * nnz
 #define CBG_HASH_LOAD_NUM 3  // 3/2: +4.6 % at scale 22 over 2/1 (more hash slabs in the smaller, higher-occupancy classes)
@@ -1307,7 +1293,8 @@ __device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank
   const int w = d.w;
   if (w & SLAB_SPARSE) {
     const int c = w & SLAB_CNT_MASK;
-    if (c > rank_min && d.y - d.x <= rank_span) return SLAB_RANK0 + (c <= 1024 ? 0 : c <= 2048 ? 1 : 2);
+    if (c > rank_min && rank_span > 0 && d.y - d.x <= rank_span)
+      return SLAB_RANK0 + (c <= 1024 ? 0 : c <= 2048 ? 1 : 2);
     int k = 0;
     while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
     return 2 + k;
@@ -1368,7 +1355,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
                             SlabRec* __restrict__ list,
                             const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
                             const int64_t* __restrict__ colptr, const int* __restrict__ gbm_slot, int plog,
-                            int64_t m_rows) {
+                            int64_t m_rows, const int* __restrict__ pcoff) {
   extern __shared__ int lsh[];  // lc[NK] | lb[NK]
   const int KR = slab_kr(R), NK = SLAB_NCLS * KR;
   int* lc = lsh;
@@ -1411,8 +1398,9 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
       rec.slot = gbm_slot ? gbm_slot[br] : -1;
       // a pair's only slab holds every row its products reach (the plan trims
       // empty fine ranges only), so A's whole panel runs are its products
-      rec.full = (d.x == R0 && d.y == R1) || nslab[br] == 1;
-      rec.ends = (s == 0 ? 1 : 0) | (s == nslab[br] - 1 ? 2 : 0);
+      const bool full = (d.x == R0 && d.y == R1) || nslab[br] == 1;
+      rec.flags = (s == 0 ? 1 : 0) | (s == nslab[br] - 1 ? 2 : 0) | (full ? SLAB_FULL : 0) | (s << 3);
+      rec.coff = pcoff ? pcoff[br] : -1;
       list[lb[key] + atomicAdd(&lc[key], 1)] = rec;
     }
   }
@@ -1879,66 +1867,6 @@ __global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64
 }
 
 // numeric: block per column
-template <int LOGT, int BS>
-struct NumBlockLds {
-  static constexpr int T = 1 << LOGT;
-  static constexpr int NB = 1024;  // buckets of the sorted emit
-  static constexpr int BYTES = T * 8 + BS * 8 + T * 4 + (BS + 4) * 4 + BS * 4 + (BS / WAVE + 4) * 4 +
-                               (2 * NB + 4) * 4 + (T / 2) * 2;
-};
-
-template <int LOGT, int BS, int SR>
-__global__ __launch_bounds__(BS) void k_num_block(const int32_t* __restrict__ perm, const int64_t* __restrict__ cpB,
-                                                  const int32_t* __restrict__ irB, const double* __restrict__ valB,
-                                                  const int2* __restrict__ cmap, const int32_t* __restrict__ irA,
-                                                  const double* __restrict__ valA, const int64_t* __restrict__ colptr,
-                                                  int32_t* __restrict__ out_ir, double* __restrict__ out_val,
-                                                  int bshift) {
-  constexpr int T = 1 << LOGT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* vals = reinterpret_cast<double*>(smem);
-  double* bv = vals + T;
-  int* keys = reinterpret_cast<int*>(bv + BS);
-  int* pref = keys + T;
-  int* st = pref + BS + 4;
-  int* tmp = st + BS;
-  const int tid = threadIdx.x;
-  const int col = perm[blockIdx.x];
-  for (int j = tid; j < T; j += BS) {
-    keys[j] = EMPTY_KEY;
-    vals[j] = Sem<SR>::identity();
-  }
-  __syncthreads();
-  const int64_t p1 = cpB[col + 1];
-  for (int64_t c0 = cpB[col]; c0 < p1; c0 += BS) {
-    const int64_t p = c0 + tid;
-    int s = 0, len = 0;
-    double bval = 0.0;
-    if (p < p1) {
-      int2 e = cmap[irB[p]];
-      s = e.x;
-      len = e.y;
-      bval = valB[p];
-    }
-    int total;
-    const int ex = block_excl_scan<BS>(len, tmp, &total);
-    pref[tid] = ex;
-    if (tid == BS - 1) pref[BS] = total;
-    st[tid] = seg_stage(s, ex);
-    bv[tid] = bval;
-    __syncthreads();
-    block_products<BS>(
-        pref, total, [&](int sg) { return SegV{seg_off(st, pref, sg), bv[sg]}; },
-        [&](const SegV& g, int u) { return RowVal{irA[g.off + u], Sem<SR>::mul(valA[g.off + u], g.b)}; },
-        [&](const RowVal& x) { hash_acc<SR, LOGT>(keys, vals, x.row, x.v); });
-    __syncthreads();
-  }
-  constexpr int NB = NumBlockLds<LOGT, BS>::NB;
-  int* boff = tmp + BS / WAVE + 4;
-  int* cur = boff + NB + 4;
-  unsigned short* members = reinterpret_cast<unsigned short*>(cur + NB);
-  hash_emit_sorted<T, BS, NB>(keys, vals, 0, bshift, boff, cur, members, tmp, out_ir, out_val, colptr[col]);
-}
 
 // numeric: one row slab of a big column by bitmap + rank.
 // Pass 1 marks the slab's rows in an LDS bitmap, a scan turns the bitmap into
@@ -2012,7 +1940,8 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                                  int64_t nA1, const int32_t* __restrict__ irA,
                                                  const VA* __restrict__ valA,
                                                  int32_t* __restrict__ out_ir,
-                                                 double* __restrict__ out_val, const unsigned* __restrict__ gbm) {
+                                                 double* __restrict__ out_val, const unsigned* __restrict__ gbm,
+                                                 const int* __restrict__ cuts) {
   // Persistent blocks (one per CU at this LDS size) pull slabs from a queue.
   // With one block per CU nothing else hides a slab's dependent global reads,
   // so the next slab's record, kept bitmap words and B staging (irB/valB,
@@ -2041,7 +1970,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   double p_bv = 0.0;
   int2 p_ce = make_int2(0, 0);
   auto rec_words = [&](const SlabRec& r) { return (r.hi - r.lo + 31) >> 5; };
-  auto staged = [&](const SlabRec& r) { return r.full && r.nb <= BS; };
+  auto staged = [&](const SlabRec& r) { return (r.flags & SLAB_FULL) && r.nb <= BS; };
   auto fetch_words = [&](const SlabRec& r) {
     if (r.slot < 0) return;
     const unsigned* src = gbm + (int64_t)r.slot * wslot + ((r.lo - (r.r << plog)) >> 5);
@@ -2082,9 +2011,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const bool pre = staged(rec);        // chunk 0 staging came in registers
     if ((c_dbg & 32) && tid == 0) {
       atomicAdd(&g_stat[0], 1ull);
-      atomicAdd(&g_stat[1], rec.full ? 0ull : 1ull);
+      atomicAdd(&g_stat[1], (rec.flags & SLAB_FULL) ? 0ull : 1ull);
       atomicAdd(&g_stat[2], (unsigned long long)rec.nb);
-      atomicAdd(&g_stat[3], rec.full ? 0ull : (unsigned long long)rec.nb);
+      atomicAdd(&g_stat[3], (rec.flags & SLAB_FULL) ? 0ull : (unsigned long long)rec.nb);
       atomicAdd(&g_stat[5], (unsigned long long)rec.nout);
       atomicAdd(&g_stat[6], rec.nb > BS ? 1ull : 0ull);
     }
@@ -2168,13 +2097,23 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           double bval = 0.0;
           if (p < p1) {
             const int2 ce = cm[irB[p]];
-            if (rec.full) {
+            if (rec.flags & SLAB_FULL) {
               s = ce.x;
               len = ce.y - ce.x;
             } else if (ce.y > ce.x) {
-              // the pair's first slab starts at its run's start, the last ends at its end
-              const int a = (rec.ends & 1) ? ce.x : lower_bound_g(irA, ce.x, ce.y, lo);
-              const int z = (rec.ends & 2) ? ce.y : lower_bound_g(irA, a, ce.y, hi);
+              // the pair's first slab starts at its run's start, the last ends at
+              // its end; the cuts between are the symbolic's (offsets into the
+              // run, cuts[coff + (slab - 1) * nb + entry]) or searched here
+              int a, z;
+              if (rec.coff >= 0) {
+                const int si = rec.flags >> 3;
+                const int64_t j = p - p0;
+                a = (rec.flags & 1) ? ce.x : ce.x + cuts[(int64_t)rec.coff + (int64_t)(si - 1) * rec.nb + j];
+                z = (rec.flags & 2) ? ce.y : ce.x + cuts[(int64_t)rec.coff + (int64_t)si * rec.nb + j];
+              } else {
+                a = (rec.flags & 1) ? ce.x : lower_bound_g(irA, ce.x, ce.y, lo);
+                z = (rec.flags & 2) ? ce.y : lower_bound_g(irA, a, ce.y, hi);
+              }
               s = a;
               len = z - a;
             }
@@ -2900,18 +2839,6 @@ static void launch_num_wave(const int32_t* perm, int n, const cbg_tile& B, const
   hipLaunchKernelGGL((k_num_wave<LOGT, SR>), dim3(nblk(n, 4)), dim3(256), lds, s, perm, n, B.cp, B.ir, B.val, cmap,
                      A.ir, A.val, colptr, C.ir, C.val);
 }
-template <int LOGT, int BS, int SR>
-static void launch_num_block(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap, const cbg_tile& A,
-                             const int64_t* colptr, cbg_tile& C, hipStream_t s) {
-  if (n <= 0) return;
-  const size_t lds = NumBlockLds<LOGT, BS>::BYTES;
-  set_lds(k_num_block<LOGT, BS, SR>, lds);
-  int lm = 0;
-  while ((1LL << lm) < A.m) ++lm;
-  const int bshift = std::max(0, lm - 10);  // NumBlockLds::NB = 2^10 buckets over [0, m)
-  hipLaunchKernelGGL((k_num_block<LOGT, BS, SR>), dim3(n), dim3(BS), lds, s, perm, B.cp, B.ir, B.val, cmap, A.ir,
-                     A.val, colptr, C.ir, C.val, bshift);
-}
 
 // records of the block hash bins: a column is a hash slab over all rows
 __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int64_t* __restrict__ cpB,
@@ -2928,8 +2855,8 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
   r.hi = m;  // the rows the slab spans
   r.nout = (int)(colptr[col + 1] - r.obase);
   r.slot = -1;
-  r.full = 1;
-  r.ends = 3;
+  r.flags = 3 | SLAB_FULL;
+  r.coff = -1;
   rec[i] = r;
 }
 
@@ -2974,6 +2901,7 @@ struct BigPlan {
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
   const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
   const PackedRV* valAp = nullptr;  // ... and as (row, f32) records (CBG_APACK)
+  DBuf<int> cuts, pcoff;  // multi-slab pairs' cut positions (sym_pair), per-pair offsets
 };
 
 
@@ -3016,7 +2944,7 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
     }
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                       A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p);
+                       A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p, bp.cuts.p);
   };
   static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
   if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV>, bp.valAp, per_cu_p);
@@ -3049,6 +2977,12 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
   df.take(queue);
 }
 
+// CBG_CUTS=0: the numeric bitmap slabs of multi-slab pairs search their cuts
+// (before round 5) instead of reading the symbolic's
+static bool cuts_enabled() {
+  static const char* e = getenv("CBG_CUTS");
+  return !(e && !strcmp(e, "0"));
+}
 // hash-mode single-panel slabs of more than this many nonzeros run as rank
 // slabs (CBG_RANK_MIN overrides; < 0: none)
 static int rank_slabs_min() {
@@ -3057,12 +2991,6 @@ static int rank_slabs_min() {
 }
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
-// bit c: hash slab class c (CBG_HASH_TABLES order) runs on the side stream
-// (CBG_SIDE_HASH overrides)
-static int side_hash_classes() {
-  static const char* e = getenv("CBG_SIDE_HASH");
-  return e ? (int)strtol(e, nullptr, 0) : 0;
-}
 
 template <int SR>
 static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp, const cbg_tile& A,
@@ -3073,11 +3001,9 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
     at[c] = list + o;
     o += ncls[c];
   }
-  // hash classes whose bit is set in side_hash_classes() queue behind the
-  // small-column bins on the side stream, so that they fill its tail while
-  // the main stream still runs the bitmap slabs
-  const int sm = side_hash_classes();
-  auto hs = [&](int c) { return (sm >> c) & 1 ? side : s; };
+  // (hash classes queued behind the small-column bins on the side stream were
+  // 3-4 % slower at scale 22: every slab class runs on the main stream)
+  auto hs = [&](int) { return s; };
   launch_slab_bitmap<SR, SLAB_SMALL_CAP, SLAB_SMALL_BS>(at[0], ncls[0], bp, A, B, C, s, df);
   launch_slab_bitmap<SR, SLAB_LARGE_CAP, SLAB_LARGE_BS>(at[1], ncls[1], bp, A, B, C, s, df);
   static_assert(SLAB_HASH_NCLS == 9, "hash slab classes (CBG_HASH_TABLES)");
@@ -3107,7 +3033,7 @@ static int gbm_min_products() {
 // by the LDS hash, before round 5)
 static int sym_pair_bitmap() {
   static const char* e = getenv("CBG_SYM_PAIR_BM");
-  return e && !strcmp(e, "1");
+  return !(e && !strcmp(e, "0"));
 }
 
 // kept symbolic bitmaps (32 KiB per (column, panel) pair): CBG_BITMAP_BUDGET_GB,
@@ -3139,6 +3065,12 @@ struct Binned {
 // pageable memory is staged by the runtime and holds the host thread once per
 // copy: ~20 us each, several per multiply): slot k of the calling thread's
 // page, read after the caller's next synchronization.
+// Rule: at most ONE local multiply per host thread has readbacks in flight at a
+// time -- the slots are fixed per thread and each is read right after the
+// synchronization that follows its copy (every caller runs its multiply to
+// completion on the thread, through its 4 host syncs, before the next one
+// starts).  An asynchronous or nested multiply on one thread would need a page
+// of its own.  The page lives for the thread (8 x 4 KiB pinned).
 static char* host_stage(int slot) {
   static thread_local char* p = nullptr;
   if (!p) CBG_HIP(hipHostMalloc((void**)&p, 8 * 4096, hipHostMallocDefault));
@@ -3218,12 +3150,6 @@ static int pick_panel_log(int64_t m) {
   return l;
 }
 
-// block hash bins through the persistent record-driven hash kernel
-// (CBG_BLOCK_BINS=classic selects the one-block-per-column k_num_block)
-static bool block_bins_persistent() {
-  static const char* e = getenv("CBG_BLOCK_BINS");
-  return !(e && !strcmp(e, "classic"));
-}
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* valAf, const cbg_tile& B,
@@ -3235,17 +3161,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* v
   launch_num_wave<7, SR>(at(2), nb.count[2], B, cmap, A, colptr, C, sb[2]);
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, sb[3]);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, sb[4]);
-  if (block_bins_persistent()) {
-    launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, sb[5], df);
-    launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, sb[6], df);
-    launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, sb[7], df);
-    launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, sb[8], df);
-  } else {
-    launch_num_block<10, 256, SR>(at(5), nb.count[5], B, cmap, A, colptr, C, sb[5]);
-    launch_num_block<11, 256, SR>(at(6), nb.count[6], B, cmap, A, colptr, C, sb[6]);
-    launch_num_block<12, 512, SR>(at(7), nb.count[7], B, cmap, A, colptr, C, sb[7]);
-    launch_num_block<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, colptr, C, sb[8]);
-  }
+  launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, sb[5], df);
+  launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, sb[6], df);
+  launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, sb[7], df);
+  launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, sb[8], df);
 }
 
 // Stream of each small-column bin: the big columns run on the main stream,
@@ -3256,7 +3175,7 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* v
 static void balance_bins(const std::vector<unsigned long long>& fl, int first, int last, double main_work,
                          double side_work, const double* cost, hipStream_t main, hipStream_t side,
                          hipStream_t* out) {
-  static const int bal = getenv("CBG_BALANCE") ? atoi(getenv("CBG_BALANCE")) : 0;  // 1: GalerkinNew 10.0 -> 9.9-10.2 ms (the streams share one saturated GPU): off
+  constexpr int bal = 0;  // balancing both streams: GalerkinNew 10.0 -> 9.9-10.2 ms (they share one saturated GPU): off
   for (int b = last; b >= first; --b) {
     const double w = (double)fl[b] * (cost ? cost[b] : 1.0);
     if (!bal || side == main || side_work <= main_work) {
@@ -3322,17 +3241,6 @@ __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __res
 static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned char* clen8, bool A_one_per_col,
                          int64_t* flops, hipStream_t s, DeferredFree& df) {
   const int64_t nz = B.nzc;
-  static const bool classic = getenv("CBG_FLOPS_CLASSIC") && atoi(getenv("CBG_FLOPS_CLASSIC"));
-  if (classic) {  // a lane group per column + hub tail (before round 3)
-    CBG_HIP(hipMemsetAsync(flops + nz, 0, sizeof(int64_t), s));
-    DBuf<int> longq(nz + 1);  // count | queued columns
-    CBG_HIP(hipMemsetAsync(longq.p, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_flops, dim3(nblk(nz * FLOP_G, 256)), dim3(256), 0, s, nz, B.cp, B.ir, cmap, flops, longq.p);
-    hipLaunchKernelGGL(k_flops_tail, dim3((unsigned)std::min<int64_t>(nz, 1024)), dim3(256), 0, s, B.cp, B.ir, cmap,
-                       nz, flops, longq.p);
-    df.take(longq);
-    return;
-  }
   if (A_one_per_col) {
     // every A column holds exactly one entry (a restriction operator's
     // transpose, GalerkinNew's S): flops(j) = nnz(B(:, j)), no gathers
@@ -3497,10 +3405,16 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   Binned sb;
   const int64_t big = big_flops(A.m);
   {
+    // once per device (c_dbg exists once per device; a pageable copy holds the host ~20 us)
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
-    static thread_local bool dbg_set = false;  // once (a pageable copy holds the host ~20 us)
-    if (!dbg_set && dbg) CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
-    dbg_set = true;
+    static std::atomic<unsigned long long> dbg_set{0};
+    if (dbg) {
+      int dev = 0;
+      CBG_HIP(hipGetDevice(&dev));
+      const unsigned long long bit = 1ull << (dev & 63);
+      if (!(dbg_set.fetch_or(bit) & bit))
+        CBG_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_dbg), &dbg, sizeof(int), 0, hipMemcpyHostToDevice, s));
+    }
   }
   // symbolic bins: kSymThr (clipped at `big`), then the big columns by panel
   // group size 2^GROUP_LOG_MAX .. 1 (columns with F * g / R <= GROUP_PRODUCTS
@@ -3514,7 +3428,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // (default 2: also those of more than `big` flops -- R-MAT columns whose one
   // entry hits a hub -- instead of (column, panel) pairs: s22 446.4 -> 440.9 ms;
   // 1: only the small ones)
-  static const int copy1 = getenv("CBG_COPY1") ? atoi(getenv("CBG_COPY1")) : 2;
+  constexpr int copy1 = 2;
   bp.plog = pick_panel_log(A.m);
   bp.R = (int)((A.m + (1LL << bp.plog) - 1) >> bp.plog);
   constexpr int NSMALL = 13, NGCLS = GROUP_LOG_MAX + 1, THIN_BIN = NSMALL + NGCLS;
@@ -3522,23 +3436,20 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   int thin_R = 0;
   {
     static const char* eg = getenv("CBG_GROUPS");
-    static const char* ep = getenv("CBG_GROUP_PRODUCTS");
     const bool groups = !(eg && !strcmp(eg, "0"));
-    const int64_t gp = ep ? atoll(ep) : GROUP_PRODUCTS;
+    const int64_t gp = GROUP_PRODUCTS;
     int64_t thr[NSMALL + NGCLS];
     for (int i = 0; i < NSMALL; ++i) thr[i] = std::min(kSymThr[i], big);
     thr[NSMALL + NGCLS - 1] = INT64_MAX;  // the single-panel big columns; bin NSMALL + NGCLS: thin ones
-    static const char* el = getenv("CBG_GROUP_LOG_MAX");
-    const int glmax = el ? std::max(0, std::min(GROUP_LOG_MAX, atoi(el))) : GROUP_LOG_MAX;
+    const int glmax = GROUP_LOG_MAX;
     for (int c = 0; c + 1 < NGCLS; ++c) {
       const int64_t g = 1LL << (GROUP_LOG_MAX - c);
       thr[NSMALL + c] = (groups && g <= bp.R && g <= (1LL << glmax)) ? gp * bp.R / g : -1;
     }
     BinPending sp;
     const bool thin_on = !(getenv("CBG_THIN") && !strcmp(getenv("CBG_THIN"), "0"));  // read per call (tests)
-    // CBG_THIN_RATIO (default 4): thin when flops * ratio < B entries * R
-    const char* tr = getenv("CBG_THIN_RATIO");
-    const int ratio = tr ? std::max(1, atoi(tr)) : (int)THIN_RATIO;
+    // thin when flops * THIN_RATIO < B entries * R (1 and 2 measured equal at scales 22/24)
+    const int ratio = (int)THIN_RATIO;
     thin_R = (fused && thin_on && bp.R >= 4) ? (int)(bp.R * THIN_RATIO / ratio) : 0;
     bin_classify(nz, flops.p, cnt.p, 0, thr, NSMALL + NGCLS, big, sp, s, 0, B.cp, NSMALL, thin_R, THIN_BIN, copy1);
     CBG_HIP(hipStreamSynchronize(s));  // host sync 1 of 4: the symbolic bins' sizes
@@ -3662,7 +3573,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
-    static const int pm_entries = getenv("CBG_PMAP_ENTRIES") ? atoi(getenv("CBG_PMAP_ENTRIES")) : 64;
+    constexpr int pm_entries = 64;  // map only the referenced A columns when big-column entries * 64 < A's columns
     if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
       bp.cmapP = ap.cmapP.p;
     } else if (bp.R > 1 && pm_entries > 0 && big_entries * pm_entries < A.nzc) {
@@ -3704,6 +3615,18 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       CBG_HIP(hipMemsetAsync(gbm_next.p, 0, sizeof(int), s));
     }
     if (nbr >= (int64_t)INT32_MAX) throw HipError("too many (column, panel) pairs", CBG_ERR_NOTSUPPORTED);
+    // the multi-slab pairs' cut positions, handed out by an atomic counter up to
+    // a budget (pairs past it leave their cuts to the numeric's searches)
+    DBuf<unsigned long long> cuts_next;
+    long long cuts_cap = 0;
+    if (!sym_only && cuts_enabled()) {
+      cuts_cap = std::min<long long>(INT32_MAX, (long long)(std::min(1.5e9, 0.02 * device_bytes_available()) / 4));
+      bp.cuts.reset(std::max<long long>(cuts_cap, 1));
+      bp.pcoff.reset(nbr);
+      cuts_next.reset(1);
+      CBG_HIP(hipMemsetAsync(bp.pcoff.p, 0xff, sizeof(int) * nbr, s));
+      CBG_HIP(hipMemsetAsync(cuts_next.p, 0, sizeof(unsigned long long), s));
+    }
     const int pwords = 1 << (bp.plog - 5);
     auto lds_of = [&](int hw) {
       return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4 +
@@ -3712,7 +3635,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
-                    bp.gbm_slot.p, gbm_min_products(), sym_pair_bitmap()};
+                    bp.gbm_slot.p, gbm_min_products(), sym_pair_bitmap(),
+                    bp.cuts.p, cuts_next.p, cuts_cap,
+                    bp.pcoff.p};
     // one launch per group class (largest groups first)
     for (int c = 0; c < NGCLS; ++c) {
       const int nc = sb.count[NSMALL + c];
@@ -3840,7 +3765,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 2 * NK * sizeof(int), s, nbig, bp.R,
                        bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p + NK, slist.p,
                        bp.perm_big, B.cp, colptr.p,
-                       bp.gbm_slot.p, bp.plog, A.m);
+                       bp.gbm_slot.p, bp.plog, A.m, bp.pcoff.p);
     int* ncls_h = reinterpret_cast<int*>(host_stage(STAGE_SLABS));
     CBG_HIP(hipMemcpyAsync(ncls_h, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));  // host sync 3 of 4: the slab classes' sizes
@@ -3881,12 +3806,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) fused_w += 0.25 * (double)sb.flops[b];
     numst[0] = numst[9] = snum;
     balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst);
-    // CBG_NUM_MAIN: bit b puts numeric bin b on the main stream, ahead of the
-    // slabs (a bin whose LDS table cannot sit beside the persistent bitmap
-    // slabs otherwise waits for them on the side stream and runs after them)
-    static const int num_main = getenv("CBG_NUM_MAIN") ? (int)strtol(getenv("CBG_NUM_MAIN"), nullptr, 0) : 0;
-    for (int b = 1; b <= 8; ++b)
-      if ((num_main >> b) & 1) numst[b] = s;
   }
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);

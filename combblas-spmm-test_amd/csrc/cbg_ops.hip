@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void k_copy16_flat(const uint4* __restrict__ s
 // shapes (grid-stride with 4 loads in flight, nontemporal or not; one launch
 // streaming the buffer with 1 / 4 / 8 loads per lane), swept on the first call
 // and the winner reused (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).
-// CBG_COPY_VARIANT=k forces shape k.  Bytes moved = 2 x the buffer.
+// Bytes moved = 2 x the buffer.
 double hbm_copy_gbps(int64_t bytes, int reps) {
   const int64_t n = std::max<int64_t>(bytes / 16, 1);
   DBuf<uint4> ba(n), bb(n);  // from the pool (it drops its cache and retries when the device is full)
@@ -340,8 +340,6 @@ double hbm_copy_gbps(int64_t bytes, int reps) {
     return 2.0 * 16.0 * (double)n * r_ / (ms * 1e-3) / 1e9;
   };
   static int best = -1;
-  static const char* ev = getenv("CBG_COPY_VARIANT");
-  if (ev) best = std::max(0, std::min(NV - 1, atoi(ev)));
   double gbps = 0.0;
   if (best < 0) {
     for (int v = 0; v < NV; ++v) {

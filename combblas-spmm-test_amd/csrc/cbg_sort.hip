@@ -165,7 +165,8 @@ __global__ void k_rbk_runs(const K* __restrict__ k, const double* __restrict__ v
 }  // namespace
 
 template <typename K>
-void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned long long varying, hipStream_t s) {
+void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned long long varying, hipStream_t s,
+                      DeferredFree* df) {
   if (n <= 1) return;
   const int64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
   DBuf<K> k2(n);
@@ -175,40 +176,52 @@ void radix_sort_pairs(DBuf<K>& keys, DBuf<double>& vals, int64_t n, unsigned lon
   for (int shift = 0; shift < (int)(8 * sizeof(K)); shift += 8) {
     if (!((varying >> shift) & 0xFFull)) continue;
     hipLaunchKernelGGL(k_rs_hist<K>, dim3((unsigned)ntiles), dim3(RS_BS), 0, s, keys.p, n, shift, ntiles, counts.p);
-    exclusive_scan_i32_to_i64(counts.p, offs.p, ntiles * RS_RADIX, s);
+    exclusive_scan_i32_to_i64(counts.p, offs.p, ntiles * RS_RADIX, s, df);
     hipLaunchKernelGGL(k_rs_scatter<K>, dim3((unsigned)ntiles), dim3(RS_BS), 0, s, keys.p, vals.p, n, shift, ntiles,
                        offs.p, k2.p, v2.p);
     std::swap(keys.p, k2.p);
     std::swap(vals.p, v2.p);
+  }
+  if (df) {  // the temporaries go back to the pool after the caller's synchronization
+    df->take(k2);
+    df->take(v2);
+    df->take(counts);
+    df->take(offs);
+    return;
   }
   CBG_HIP(hipStreamSynchronize(s));  // k2 / v2 / counts go back to the pool
 }
 
 template <typename K>
 int64_t reduce_by_key(const K* keys, const double* vals, int64_t n, int semiring, K* ukeys, double* uvals,
-                      hipStream_t s) {
+                      hipStream_t s, DeferredFree* df) {
   if (n <= 0) return 0;
   DBuf<int32_t> flag(n + 1);
   DBuf<int64_t> pos(n + 1);
   const unsigned g = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(k_rbk_flags<K>, dim3(g), dim3(256), 0, s, keys, n, flag.p);
-  exclusive_scan_i32_to_i64(flag.p, pos.p, n, s);
+  exclusive_scan_i32_to_i64(flag.p, pos.p, n, s, df);
   if (semiring == CBG_MIN_PLUS)
     hipLaunchKernelGGL((k_rbk_runs<K, 1>), dim3(g), dim3(256), 0, s, keys, vals, n, pos.p, ukeys, uvals);
   else
     hipLaunchKernelGGL((k_rbk_runs<K, 0>), dim3(g), dim3(256), 0, s, keys, vals, n, pos.p, ukeys, uvals);
   int64_t runs = 0;
   CBG_HIP(hipMemcpyAsync(&runs, pos.p + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  CBG_HIP(hipStreamSynchronize(s));
+  CBG_HIP(hipStreamSynchronize(s));  // the one readback: the run count
+  if (df) {
+    df->take(flag);
+    df->take(pos);
+  }
   return runs;
 }
 
-template void radix_sort_pairs<uint32_t>(DBuf<uint32_t>&, DBuf<double>&, int64_t, unsigned long long, hipStream_t);
+template void radix_sort_pairs<uint32_t>(DBuf<uint32_t>&, DBuf<double>&, int64_t, unsigned long long, hipStream_t,
+                                         DeferredFree*);
 template void radix_sort_pairs<unsigned long long>(DBuf<unsigned long long>&, DBuf<double>&, int64_t,
-                                                   unsigned long long, hipStream_t);
+                                                   unsigned long long, hipStream_t, DeferredFree*);
 template int64_t reduce_by_key<uint32_t>(const uint32_t*, const double*, int64_t, int, uint32_t*, double*,
-                                         hipStream_t);
+                                         hipStream_t, DeferredFree*);
 template int64_t reduce_by_key<unsigned long long>(const unsigned long long*, const double*, int64_t, int,
-                                                   unsigned long long*, double*, hipStream_t);
+                                                   unsigned long long*, double*, hipStream_t, DeferredFree*);
 
 }  // namespace cbg

@@ -640,6 +640,9 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   // rest is broadcast at once and the pieces are rejoined into one multiply
   // (rule 3).
   if (np == 2 && adaptive && !g->host_mode && pr >= 3) info.rule = 1;
+  // several pieces without the adaptive decision (CBG_PIPELINE, or the phases
+  // of MemEfficientSpGEMM given as pieces): a fixed pipeline (rule 4)
+  if (np > 1 && !adaptive) info.rule = 4;
   if (adaptive && np == 2 && !local && info.rule == 0) {
     float ms0 = 0.f;
     local = step([&] {

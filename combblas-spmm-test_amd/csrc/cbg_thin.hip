@@ -169,8 +169,8 @@ void thin_impl(const int32_t* perm, int n, int64_t E, int64_t fthin, const cbg_t
   }
 #undef CBG_THIN_EXPAND
   const int end_bit = rowbits + colbits;
-  radix_sort_pairs<K>(k0, v0, fthin, end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1, s);
-  const int64_t nruns = reduce_by_key<K>(k0.p, v0.p, fthin, semiring, uk.p, tval + base, s);
+  radix_sort_pairs<K>(k0, v0, fthin, end_bit >= 64 ? ~0ull : (1ull << end_bit) - 1, s, &df);
+  const int64_t nruns = reduce_by_key<K>(k0.p, v0.p, fthin, semiring, uk.p, tval + base, s, &df);
   hipLaunchKernelGGL(k_thin_rows<K>, dim3((unsigned)((nruns + 255) / 256)), dim3(256), 0, s, uk.p, nruns, rowbits,
                      tir + base, first.p);
   hipLaunchKernelGGL(k_thin_slots, dim3((n + 255) / 256), dim3(256), 0, s, perm, n, first.p, nruns, base, cnt,

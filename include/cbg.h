@@ -173,7 +173,8 @@ int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);
 int cbg_last_summa_info(int* pieces, double* bcast_ms_piece0, double* est_hidden_ms, double* piece_cost_ms);
 /* ... and its communication: the double-buffering rule applied (0 one piece,
  * 1 pipelined because the B block column has > 1 remote tile on an RCCL grid,
- * 2 adaptive and pipelined, 3 adaptive and rejoined), the bytes of the remote
+ * 2 adaptive and pipelined, 3 adaptive and rejoined, 4 a fixed pipeline of
+ * several pieces: CBG_PIPELINE or phases given as pieces), the bytes of the remote
  * A and B tiles this rank received, and the exposed communication: the summed
  * ms the compute stream waited for broadcasts (HIP events around each wait) */
 int cbg_last_summa_comm(int* rule, int64_t* bytes_recv, double* exposed_comm_ms);

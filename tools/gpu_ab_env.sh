@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of environment settings on ONE build (the in-tree libcbg.so):
-#   TESTS_K="expr" (optional) runs that pytest -k selection of test_gpu_local.py first;
+#   TESTS_K="expr" (optional) runs that pytest -k selection of test_gpu_local.py first
+#   (under TESTS_ENV="VAR=x,VAR2=y" when given);
 #   ENVS="name1:VAR=x,VAR2=y name2:VAR=z base:" benches each setting ROUNDS times (interleaved),
 #   bench.py --scale ${SCALE:-22} --steps ${STEPS:-5} ${BENCH_ARGS}; DBG_ENV (optional) = the
 #   setting whose CBG_DBG=48 phase/stat lines are printed at the end.
@@ -8,7 +9,7 @@ set -o pipefail
 out=gpurun_out/${OUT:-abenv}
 mkdir -p $out
 if [ -n "$TESTS_K" ]; then
-  timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest tests/test_gpu_local.py -x -q --timeout 300 --timeout-method thread \
+  env $(echo $TESTS_ENV | tr ',' ' ') timeout -k 10 ${TESTS_TIMEOUT:-600} python -u -m pytest tests/test_gpu_local.py -x -q --timeout 300 --timeout-method thread \
     -k "$TESTS_K" > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
   tail -1 $out/tests.log
 fi

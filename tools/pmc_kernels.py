@@ -25,9 +25,13 @@ if __name__ == "__main__":
         for k, c in load(p).items():
             agg[k].update(c)
     names = sorted({c for v in agg.values() for c in v})
-    top = sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", kv[1].get("SQ_BUSY_CYCLES", 0)))[:10]
+    def weight(c):
+        return c.get("SQ_WAVE_CYCLES", c.get("SQ_BUSY_CYCLES", c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0)))
+    top = sorted(agg.items(), key=lambda kv: -weight(kv[1]))[:14]
     for k, c in top:
         wc = max(c.get("SQ_WAVE_CYCLES", 1), 1)
-        print(f"== {k}")
+        hit = c.get("TCC_HIT_sum", 0.0)
+        miss = c.get("TCC_MISS_sum", 0.0)
+        print(f"== {k}" + (f"   L2 hit {hit / (hit + miss):.3f}" if hit + miss > 0 else ""))
         print("   " + "  ".join(f"{n}={c[n]:.3g}" + (f"({c[n]/wc:.2f}wc)" if n.startswith(("SQ_WAIT", "SQ_ACTIVE")) else "")
                                for n in names if n in c))
