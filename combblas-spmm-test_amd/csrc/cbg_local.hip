@@ -630,6 +630,34 @@ __global__ void k_colmap_panels_entries(const int32_t* __restrict__ perm_big, in
   }
 }
 
+// Panel-blocked copy of A's rows (CBG_APB=1) for the symbolic's single-panel
+// units: panel 0's rows of every column, then panel 1's, ...; cmapB[r][k] =
+// (first, end) of A(:,k)'s panel-r run in the copy.  Column-major, a column's
+// ~16 rows (scale 22) share one 64-byte line, so a pass over one panel touches
+// every column's line: all of irA (256 MB) per panel.  Blocked, a panel's runs
+// are contiguous (16 MB).  Panel groups keep the column-major rows.
+__global__ void k_pb_counts(int64_t N, const int2* __restrict__ cmapP, int32_t* __restrict__ cnt) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < N) cnt[i] = cmapP[i].y - cmapP[i].x;
+}
+__global__ void k_pb_map(int64_t N, const int2* __restrict__ cmapP, const int64_t* __restrict__ off,
+                         int2* __restrict__ cmapB) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < N) cmapB[i] = make_int2((int)off[i], (int)off[i] + (cmapP[i].y - cmapP[i].x));
+}
+__global__ void k_pb_copy(int64_t nzcA, const int32_t* __restrict__ jcA, int R, int64_t nA1,
+                          const int2* __restrict__ cmapP, const int2* __restrict__ cmapB,
+                          const int32_t* __restrict__ irA, int32_t* __restrict__ irAB) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= nzcA) return;
+  const int64_t k = jcA[i];
+  for (int r = 0; r < R; ++r) {
+    const int2 e = cmapP[r * nA1 + k];
+    const int d = cmapB[r * nA1 + k].x - e.x;
+    for (int q = e.x; q < e.y; ++q) irAB[d + q] = irA[q];
+  }
+}
+
 // symbolic of the big columns, one block per (column, panel group).
 //
 // A pair (column, panel) is counted into a bitmap of the panel's rows with
@@ -669,6 +697,8 @@ struct SymPanelArgs {
   int64_t nA1;
   const int32_t* irA;
   int64_t m;
+  const int2* cmapB;    // panel-blocked map and rows of A for single-panel units (null: cmapP / irA)
+  const int32_t* irAB;
   int32_t* cnt;
   int32_t* cnt_br;
   int4* desc;
@@ -773,7 +803,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int R = a.R, plog = a.plog;
   const int64_t* __restrict__ cpB = a.cpB;
   const int32_t* __restrict__ irB = a.irB;
-  const int32_t* __restrict__ irA = a.irA;
+  const int32_t* __restrict__ irA = a.cmapB ? a.irAB : a.irA;
   int32_t* __restrict__ cnt = a.cnt;
   int32_t* __restrict__ cnt_br = a.cnt_br;
   int4* __restrict__ desc = a.desc;
@@ -794,7 +824,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int R0 = r << plog;
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), a.m);
   const int words = (R1 - R0 + 31) >> 5;
-  const int2* cm = a.cmapP + (int64_t)r * a.nA1;
+  const int2* cm = (a.cmapB ? a.cmapB : a.cmapP) + (int64_t)r * a.nA1;
   unsigned long long tmark = wall_clock64();
   const int64_t p0 = pre.ok ? pre.p0 : cpB[col], p1 = pre.ok ? pre.p1 : cpB[col + 1];
   int64_t prod = 0;  // products of the pair
@@ -1223,7 +1253,7 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
       nxt.s = nxt.len = 0;
       nxt.ok = n_p1 - n_p0 <= BS ? 2 : 1;
       if (n_k >= 0) {
-        const int2 e0 = a.cmapP[(int64_t)n_r0 * a.nA1 + n_k];
+        const int2 e0 = (a.cmapB && n_r1 == n_r0 ? a.cmapB : a.cmapP)[(int64_t)n_r0 * a.nA1 + n_k];
         const int e1y = n_r1 > n_r0 ? a.cmapP[(int64_t)n_r1 * a.nA1 + n_k].y : e0.y;
         nxt.s = e0.x;
         nxt.len = e1y - e0.x;
@@ -3199,6 +3229,8 @@ struct APrep {
   int plog = -1;
   DBuf<float> valf;  // A's values as f32 (af == 1)
   DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
+  DBuf<int2> cmapB;     // panel-blocked rows of A (CBG_APB): built with cmapP
+  DBuf<int32_t> irAB;
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
 
@@ -3260,6 +3292,11 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned cha
   df.take(c_lo);
 }
 
+// CBG_APB=1: a panel-blocked copy of A's rows for the symbolic's single-panel units
+static bool apb_enabled() {
+  static const char* e = getenv("CBG_APB");
+  return e && !strcmp(e, "1");
+}
 // CBG_APACK=0: the slab kernels read A's rows and f32 values from two arrays
 static bool apack_enabled() {
   static const char* e = getenv("CBG_APACK");
@@ -3281,6 +3318,8 @@ void aprep_end() {
   a.cmapP.release();
   a.valf.release();
   a.valp.release();
+  a.cmapB.release();
+  a.irAB.release();
   a.af = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
@@ -3373,6 +3412,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.cmapP.release();
     ap.valf.release();
     ap.valp.release();
+    ap.cmapB.release();
+    ap.irAB.release();
     ap.af = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
@@ -3574,6 +3615,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
     constexpr int pm_entries = 64;  // map only the referenced A columns when big-column entries * 64 < A's columns
+    bool pmap_full = true;  // cmapP maps every column of A (not only the referenced ones)
     if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
       bp.cmapP = ap.cmapP.p;
     } else if (bp.R > 1 && pm_entries > 0 && big_entries * pm_entries < A.nzc) {
@@ -3586,9 +3628,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       hipLaunchKernelGGL(k_colmap_panels_entries, dim3(nblk((int64_t)nbig * WAVE, 256)), dim3(256), 0, s,
                          bp.perm_big, nbig, B.cp, B.ir, cmap.p, A.ir, bp.plog, bp.R, A.n + 1, bp.cmapP_own.p);
       bp.cmapP = bp.cmapP_own.p;
+      pmap_full = false;
     } else {
       DBuf<int2>& cp = ap.active ? ap.cmapP : bp.cmapP_own;
       cp.reset((size_t)bp.R * (A.n + 1));
+      if (ap.active) {  // a blocked copy made from the previous map is stale
+        ap.cmapB.release();
+        ap.irAB.release();
+      }
       if (bp.R == 1) {
         hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, cp.p);
       } else {
@@ -3598,6 +3645,35 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       }
       if (ap.active) ap.plog = bp.plog;
       bp.cmapP = cp.p;
+    }
+    // panel-blocked rows of A for the symbolic (CBG_APB), cached like cmapP
+    const int2* cmapB = nullptr;
+    const int32_t* irAB = nullptr;
+    DBuf<int2> cmapB_own;
+    DBuf<int32_t> irAB_own;
+    if (apb_enabled() && bp.R > 1 && pmap_full) {
+      DBuf<int2>& cB = ap.active ? ap.cmapB : cmapB_own;
+      DBuf<int32_t>& iB = ap.active ? ap.irAB : irAB_own;
+      if (!(ap.active && cB.p)) {
+        const int64_t N = (int64_t)bp.R * (A.n + 1);
+        DBuf<int32_t> cnt_pb(N);
+        DBuf<int64_t> off_pb(N + 1);
+        cB.reset(N);
+        iB.reset(std::max<int64_t>(A.nnz, 1));
+        hipLaunchKernelGGL(k_pb_counts, dim3(nblk(N, 256)), dim3(256), 0, s, N, bp.cmapP, cnt_pb.p);
+        exclusive_scan_i32_to_i64(cnt_pb.p, off_pb.p, N, s, &df);
+        hipLaunchKernelGGL(k_pb_map, dim3(nblk(N, 256)), dim3(256), 0, s, N, bp.cmapP, off_pb.p, cB.p);
+        hipLaunchKernelGGL(k_pb_copy, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.jc, bp.R, A.n + 1, bp.cmapP,
+                           cB.p, A.ir, iB.p);
+        df.take(cnt_pb);
+        df.take(off_pb);
+      }
+      cmapB = cB.p;
+      irAB = iB.p;
+      if (!ap.active) {  // this call's own copy: released after the multiply
+        df.take(cmapB_own);
+        df.take(irAB_own);
+      }
     }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
     bp.nslab.reset(nbr);
@@ -3634,6 +3710,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     };
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
+                    cmapB, irAB,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p, gbm_min_products(), sym_pair_bitmap(),
                     bp.cuts.p, cuts_next.p, cuts_cap,
