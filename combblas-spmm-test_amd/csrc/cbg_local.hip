@@ -1866,33 +1866,61 @@ __global__ __launch_bounds__(256) void k_copy_single(int64_t nz, const int64_t* 
   }
 }
 
-// the single-entry columns of more than `big` flops (copy1 = 2): a block takes
-// 256 columns and copies each such column with all its threads
+// the single-entry columns of more than `big` flops (copy1 = 2): their sizes
+// (flops = the A column's length) for an exclusive scan, so that the copy can be
+// split into equal chunks.  A block per column (round 4) left a hub column of
+// ~10^5 entries to 256 threads: at scale 24 that kernel ran 80 ms per phase
+// for a few blocks (the side stream), beside k_num_slab.
+__global__ void k_single_big_sizes(int64_t nz, const int64_t* __restrict__ cpB, const int64_t* __restrict__ flops,
+                                   int64_t big, int64_t* __restrict__ sz) {
+  const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (col < nz) sz[col] = (flops[col] > big && cpB[col + 1] - cpB[col] == 1) ? flops[col] : 0;
+}
+// chunk of SB_CHUNK entries of the flattened copies (off: the scan of the
+// sizes, off[nz] = total); a chunk spans at most two columns (each holds
+// > big >= SB_CHUNK entries)
+constexpr int SB_CHUNK = 4096;
+__device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a, int64_t n, int64_t key) {
+  int64_t lo = 0, hi = n;  // first i in [0, n) with a[i] > key
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
 template <int SR>
-__global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64_t* __restrict__ cpB,
+__global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ cpB,
                                                          const int32_t* __restrict__ irB,
                                                          const double* __restrict__ valB,
                                                          const int2* __restrict__ cmap,
-                                                         const int64_t* __restrict__ flops, int64_t big,
                                                          const int32_t* __restrict__ irA,
                                                          const double* __restrict__ valA,
                                                          const int64_t* __restrict__ colptr,
                                                          int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
-  __shared__ int64_t list[256];
-  __shared__ int nlist;
-  if (threadIdx.x == 0) nlist = 0;
+  __shared__ int64_t col[2], base[2], dst[2];
+  __shared__ int src[2];
+  __shared__ double bv[2];
+  const int64_t total = off[nz];
+  const int64_t q0 = (int64_t)blockIdx.x * SB_CHUNK;
+  if (q0 >= total) return;
+  const int64_t q1 = min(q0 + SB_CHUNK, total);
+  if (threadIdx.x < 2) {
+    // the columns holding entries q0 and q1 - 1 (the last column whose offset is <= q)
+    const int64_t c = upper_bound_i64(off, nz + 1, threadIdx.x ? q1 - 1 : q0) - 1;
+    const int64_t p = cpB[c];
+    col[threadIdx.x] = c;
+    base[threadIdx.x] = off[c];
+    dst[threadIdx.x] = colptr[c];
+    src[threadIdx.x] = cmap[irB[p]].x;
+    bv[threadIdx.x] = valB[p];
+  }
   __syncthreads();
-  const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (col < nz && flops[col] > big && cpB[col + 1] - cpB[col] == 1) list[atomicAdd(&nlist, 1)] = col;
-  __syncthreads();
-  for (int l = 0; l < nlist; ++l) {
-    const int64_t c = list[l], p = cpB[c], dst = colptr[c];
-    const int2 m = cmap[irB[p]];
-    const double b = valB[p];
-    for (int e = threadIdx.x; e < m.y; e += blockDim.x) {
-      out_ir[dst + e] = irA[m.x + e];
-      out_val[dst + e] = Sem<SR>::mul(valA[m.x + e], b);
-    }
+  for (int64_t q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const int w = q >= base[1] ? 1 : 0;
+    const int64_t e = q - base[w];
+    out_ir[dst[w] + e] = irA[src[w] + e];
+    out_val[dst[w] + e] = Sem<SR>::mul(valA[src[w] + e], bv[w]);
   }
 }
 
@@ -2908,6 +2936,8 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
       CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
       if (per_cu < 1) per_cu = 1;
     }
+    // (a quarter / a 16th of the resident blocks, leaving the big-column slabs on
+    // the main stream more CUs: 424 / 537 vs 418.5 ms at scale 22)
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap,
                        (int64_t)0, A.ir, valA, C.ir, C.val);
@@ -3784,10 +3814,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   exclusive_scan_i64(flag.p, pos.p, nz, s, &df);
   CBG_HIP(hipMemcpyAsync(&scal[2], pos.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CBG_HIP(hipMemcpyAsync(&scal[3], flops.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  // single-entry big columns: their sizes' scan (the chunked copy), total read back with sync 2
+  DBuf<int64_t> sb_sz, sb_off;
+  scal[4] = 0;
+  if (copy1 > 1 && !sym_only) {
+    sb_sz.reset(nz);
+    sb_off.reset(nz + 1);
+    hipLaunchKernelGGL(k_single_big_sizes, dim3(nblk(nz, 256)), dim3(256), 0, s, nz, B.cp, flops.p, big, sb_sz.p);
+    exclusive_scan_i64(sb_sz.p, sb_off.p, nz, s, &df);
+    CBG_HIP(hipMemcpyAsync(&scal[4], sb_off.p + nz, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  }
   CBG_HIP(hipEventRecord(ev1, s));
   CBG_HIP(hipStreamSynchronize(s));  // host sync 2 of 4
   const int64_t nnzc = scal[0], nzcC = scal[2], flops_total = scal[3];
   nslabs = scal[1];
+  const int64_t single_big_entries = scal[4];
   if (sym_only) {
     df.synced = true;
     if (st) {
@@ -3902,13 +3943,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       hipLaunchKernelGGL(k_copy_single<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
                          flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
   }
-  if (copy1 > 1) {
+  if (copy1 > 1 && single_big_entries > 0) {
+    const unsigned g = (unsigned)((single_big_entries + SB_CHUNK - 1) / SB_CHUNK);
     if (semiring == CBG_MIN_PLUS)
-      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val,
-                         cmap.p, flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
+      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, B.cp, B.ir, B.val, cmap.p,
+                         A.ir, A.val, colptr.p, C.ir, C.val);
     else
-      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val,
-                         cmap.p, flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
+      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, B.cp, B.ir, B.val, cmap.p,
+                         A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
