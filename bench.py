@@ -51,7 +51,7 @@ def load_cbg():
 # (broadcast piece by piece behind the multiply); measured per rank tile on one
 # GPU: 2x1 7 % and 4x2 2-13 % faster than 1x2 / 2x4.  --grid RxC overrides.
 GRIDS = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2), 9: (3, 3), 16: (4, 4)}
-ROUND = "r04"
+ROUND = "r05"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 

@@ -673,7 +673,10 @@ __global__ void k_pb_copy(int64_t nzcA, const int32_t* __restrict__ jcA, int R, 
 // slab over the group's rows.  That shares the B column staging and column
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
 constexpr int GROUP_LOG_MAX = 6;      // groups of up to 64 panels (scale 24: R = 64 panels per column)
-constexpr int GROUP_PRODUCTS = 3072;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
+#ifndef CBG_GROUP_PRODUCTS
+#define CBG_GROUP_PRODUCTS 3072
+#endif
+constexpr int GROUP_PRODUCTS = CBG_GROUP_PRODUCTS;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
 #ifndef CBG_SYM_WAVES_OF_UNITS  // persistent symbolic grid: resident blocks x this
 #define CBG_SYM_WAVES_OF_UNITS 32  // 1: -2 % (static stride meets hub-column imbalance); 16-32: +1 % at scale 22
 #endif
