@@ -1879,9 +1879,9 @@ __global__ void k_single_big_sizes(int64_t nz, const int64_t* __restrict__ cpB, 
   const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (col < nz) sz[col] = (flops[col] > big && cpB[col + 1] - cpB[col] == 1) ? flops[col] : 0;
 }
-// chunk of SB_CHUNK entries of the flattened copies (off: the scan of the
-// sizes, off[nz] = total); a chunk spans at most two columns (each holds
-// > big >= SB_CHUNK entries)
+// chunk of ch = min(SB_CHUNK, big + 1) entries of the flattened copies (off:
+// the scan of the sizes, off[nz] = total); a chunk spans at most two columns
+// (each holds > big >= ch - 1 entries)
 constexpr int SB_CHUNK = 4096;
 __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a, int64_t n, int64_t key) {
   int64_t lo = 0, hi = n;  // first i in [0, n) with a[i] > key
@@ -1892,7 +1892,7 @@ __device__ __forceinline__ int64_t upper_bound_i64(const int64_t* __restrict__ a
   return lo;
 }
 template <int SR>
-__global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64_t* __restrict__ off,
+__global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64_t* __restrict__ off, int ch,
                                                          const int64_t* __restrict__ cpB,
                                                          const int32_t* __restrict__ irB,
                                                          const double* __restrict__ valB,
@@ -1905,9 +1905,9 @@ __global__ __launch_bounds__(256) void k_copy_single_big(int64_t nz, const int64
   __shared__ int src[2];
   __shared__ double bv[2];
   const int64_t total = off[nz];
-  const int64_t q0 = (int64_t)blockIdx.x * SB_CHUNK;
+  const int64_t q0 = (int64_t)blockIdx.x * ch;
   if (q0 >= total) return;
-  const int64_t q1 = min(q0 + SB_CHUNK, total);
+  const int64_t q1 = min(q0 + ch, total);
   if (threadIdx.x < 2) {
     // the columns holding entries q0 and q1 - 1 (the last column whose offset is <= q)
     const int64_t c = upper_bound_i64(off, nz + 1, threadIdx.x ? q1 - 1 : q0) - 1;
@@ -3947,13 +3947,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                          flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (copy1 > 1 && single_big_entries > 0) {
-    const unsigned g = (unsigned)((single_big_entries + SB_CHUNK - 1) / SB_CHUNK);
+    const int ch = (int)std::min<int64_t>(SB_CHUNK, big + 1);
+    const unsigned g = (unsigned)((single_big_entries + ch - 1) / ch);
     if (semiring == CBG_MIN_PLUS)
-      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, B.cp, B.ir, B.val, cmap.p,
-                         A.ir, A.val, colptr.p, C.ir, C.val);
+      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, ch, B.cp, B.ir, B.val,
+                         cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
     else
-      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, B.cp, B.ir, B.val, cmap.p,
-                         A.ir, A.val, colptr.p, C.ir, C.val);
+      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, ch, B.cp, B.ir, B.val,
+                         cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (nslabs > 0) {
     if (semiring == CBG_MIN_PLUS) launch_slabs<1>(slist.p, ncls, bp, A, B, C, s, side, df);
