@@ -1952,8 +1952,8 @@ struct SlabLds {
   static constexpr int BYTES = WPRE_OFF + SLAB_WORDS * 2;
   static_assert(BYTES <= 160 * 1024, "slab LDS");
 };
-#ifndef CBG_SLAB_SMALL_CAP
-#define CBG_SLAB_SMALL_CAP 2048
+#ifndef CBG_SLAB_SMALL_CAP  // the largest value array that keeps 2 blocks of 512 per CU (81856 B of LDS):
+#define CBG_SLAB_SMALL_CAP 3056  // 412.6-414.4 vs 418.2-419.4 ms at 2048 (scale 22, same box)
 #endif
 constexpr int SLAB_SMALL_CAP = CBG_SLAB_SMALL_CAP, SLAB_SMALL_BS = 512;
 constexpr int SLAB_LARGE_CAP = SLAB_CAP, SLAB_LARGE_BS = CBG_SLAB_LARGE_BS;
