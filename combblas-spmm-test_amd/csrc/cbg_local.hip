@@ -3406,12 +3406,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   TileGuard Cg;  // C's arrays until the multiply has completed (exceptions included)
   DeferredFree df;
   // side stream for the small-column bins (independent of the big columns)
-  static thread_local hipStream_t side = nullptr;
-  static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // (and a copy stream for the numeric's direct copies into C)
+  static thread_local hipStream_t side = nullptr, scopy = nullptr;
+  static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cjoin = nullptr;
   if (!side) {
     CBG_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    CBG_HIP(hipStreamCreateWithFlags(&scopy, hipStreamNonBlocking));
     CBG_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     CBG_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+    CBG_HIP(hipEventCreateWithFlags(&ev_cjoin, hipEventDisableTiming));
   }
   // CBG_SIDE=0/1/2/3: small-column bins of the symbolic (bit 0) / numeric (bit 1)
   // on the side stream (default 3), else serialized on the main stream
@@ -3421,6 +3424,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipEventRecord(ev_fork, main));
     CBG_HIP(hipStreamWaitEvent(side, ev_fork, 0));
   };
+  // CBG_COPY_STREAM=0/1: the numeric's copies behind the side stream's bins /
+  // on a stream of their own (default: their own unless the big columns dominate)
+  static const int copy_stream_env = getenv("CBG_COPY_STREAM") ? atoi(getenv("CBG_COPY_STREAM")) : -1;
   auto join = [&](hipStream_t main) {
     CBG_HIP(hipEventRecord(ev_join, side));
     CBG_HIP(hipStreamWaitEvent(main, ev_join, 0));
@@ -3572,6 +3578,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // streams of the small symbolic bins (balance_bins; the fused bins also do
   // their numeric work: cost 2 per flop)
   hipStream_t symst[NSMALL];
+  bool big_dominant = false;  // the (column, panel) units carry most of the flops over >= 8 row panels
   {
     double main_w = 0.0;
     for (int b = NSMALL; b < NSMALL + NGCLS; ++b) main_w += (double)sb.flops[b];
@@ -3585,11 +3592,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     // products (GalerkinNew) keep the concurrency (side: 6.67 vs 6.79 ms and
     // 6.37 vs 6.85 ms)
     hipStream_t sy = ssym;
-    if (!getenv("CBG_SIDE") && bp.R >= 8) {
+    if (bp.R >= 8) {
       double small_w = 0.0;
       for (int b = 1; b < NSMALL; ++b) small_w += (double)sb.flops[b];
-      if (main_w >= small_w) sy = s;
+      big_dominant = main_w >= small_w;
     }
+    if (!getenv("CBG_SIDE") && big_dominant) sy = s;
     symst[0] = sy;
     balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, sy, symst);
   }
@@ -3916,14 +3924,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // numeric
   Binned nbn;
   bin_scatter(nz, npend, nbn, s, df);
-  // small-column bins on the side stream, big-column slabs on the main one
+  // small-column bins on the side stream, big-column slabs on the main one,
+  // the copies (fused bins, single-entry columns) on the copy stream: they only
+  // need colptr and stream at HBM rate beside the latency-bound kernels
+  // (GalerkinNew at 22: 5.92 / 5.98 vs 6.45 / 6.38 ms); not where the big
+  // columns' slabs dominate, which they slow (scale 22: 418.4 vs 413.0 ms)
+  const bool copy_stream = copy_stream_env >= 0 ? copy_stream_env > 0 : !big_dominant;
   fork(s);
+  const hipStream_t sc = copy_stream ? scopy : snum;
+  if (copy_stream) CBG_HIP(hipStreamWaitEvent(scopy, ev_fork, 0));
   hipStream_t numst[10];
   {
     // the slabs of the big columns on the main stream; the fused bins' copies on
     // the side one (about a quarter of a product's cost per entry)
     double fused_w = 0.0;
-    if (fused)
+    if (fused && !copy_stream)
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) fused_w += 0.25 * (double)sb.flops[b];
     numst[0] = numst[9] = snum;
     balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst);
@@ -3932,7 +3947,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   if (fused && (fused_off[SYM_FUSED_LAST + 1] > 0 || (thin_R && sb.count[THIN_BIN] > 0)))
   {
-    hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, fused_slot.p, cnt.p,
+    hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz, 256)), dim3(256), 0, sc, nz, fused_slot.p, cnt.p,
                        colptr.p, fused_ir.p, fused_val.p, C.ir, C.val, (int64_t)fused_off[SYM_FUSED_LAST + 1]);
     if (thin_R)
       thin_copy(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], fused_slot.p, cnt.p, colptr.p, fused_ir.p,
@@ -3940,20 +3955,20 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (copy1) {
     if (semiring == CBG_MIN_PLUS)
-      hipLaunchKernelGGL(k_copy_single<1>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
+      hipLaunchKernelGGL(k_copy_single<1>, dim3(nblk(nz, 256)), dim3(256), 0, sc, nz, B.cp, B.ir, B.val, cmap.p,
                          flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
     else
-      hipLaunchKernelGGL(k_copy_single<0>, dim3(nblk(nz, 256)), dim3(256), 0, snum, nz, B.cp, B.ir, B.val, cmap.p,
+      hipLaunchKernelGGL(k_copy_single<0>, dim3(nblk(nz, 256)), dim3(256), 0, sc, nz, B.cp, B.ir, B.val, cmap.p,
                          flops.p, big, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (copy1 > 1 && single_big_entries > 0) {
     const int ch = (int)std::min<int64_t>(SB_CHUNK, big + 1);
     const unsigned g = (unsigned)((single_big_entries + ch - 1) / ch);
     if (semiring == CBG_MIN_PLUS)
-      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, ch, B.cp, B.ir, B.val,
+      hipLaunchKernelGGL(k_copy_single_big<1>, dim3(g), dim3(256), 0, sc, nz, sb_off.p, ch, B.cp, B.ir, B.val,
                          cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
     else
-      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(g), dim3(256), 0, snum, nz, sb_off.p, ch, B.cp, B.ir, B.val,
+      hipLaunchKernelGGL(k_copy_single_big<0>, dim3(g), dim3(256), 0, sc, nz, sb_off.p, ch, B.cp, B.ir, B.val,
                          cmap.p, A.ir, A.val, colptr.p, C.ir, C.val);
   }
   if (nslabs > 0) {
@@ -3961,6 +3976,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     else launch_slabs<0>(slist.p, ncls, bp, A, B, C, s, side, df);
   }
   join(s);
+  if (copy_stream) {
+    CBG_HIP(hipEventRecord(ev_cjoin, scopy));
+    CBG_HIP(hipStreamWaitEvent(s, ev_cjoin, 0));
+  }
   CBG_HIP(hipEventRecord(ev2, s));
   CBG_HIP(hipStreamSynchronize(s));  // host sync 4 of 4: C complete
   df.synced = true;
