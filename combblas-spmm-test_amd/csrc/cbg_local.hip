@@ -3235,10 +3235,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* v
 // carry less work than the small ones (GalerkinNew: 6 % of the flops), when
 // bins from the largest down go to whichever stream has less work so far, so
 // that both finish together.  Work = flops x the bin's relative cost.
+// (bal = false: every bin to the side stream)
 static void balance_bins(const std::vector<unsigned long long>& fl, int first, int last, double main_work,
                          double side_work, const double* cost, hipStream_t main, hipStream_t side,
-                         hipStream_t* out) {
-  constexpr int bal = 0;  // balancing both streams: GalerkinNew 10.0 -> 9.9-10.2 ms (they share one saturated GPU): off
+                         hipStream_t* out, bool bal = false) {
   for (int b = last; b >= first; --b) {
     const double w = (double)fl[b] * (cost ? cost[b] : 1.0);
     if (!bal || side == main || side_work <= main_work) {
@@ -3599,7 +3599,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     }
     if (!getenv("CBG_SIDE") && big_dominant) sy = s;
     symst[0] = sy;
-    balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, sy, symst);
+    balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, sy, symst, !big_dominant);
   }
   {
     const int32_t* P = sb.perm.p;
@@ -3941,7 +3941,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     if (fused && !copy_stream)
       for (int b = 1; b <= SYM_FUSED_LAST; ++b) fused_w += 0.25 * (double)sb.flops[b];
     numst[0] = numst[9] = snum;
-    balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst);
+    // balanced when the copies have their own stream (GalerkinNew 6.01 vs 6.07 ms,
+    // 3 rounds; round 3, before the copy stream: 9.9-10.2 vs 10.0 ms, off)
+    balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst, copy_stream);
   }
   if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
   else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
