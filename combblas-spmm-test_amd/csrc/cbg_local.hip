@@ -630,34 +630,6 @@ __global__ void k_colmap_panels_entries(const int32_t* __restrict__ perm_big, in
   }
 }
 
-// Panel-blocked copy of A's rows (CBG_APB=1) for the symbolic's single-panel
-// units: panel 0's rows of every column, then panel 1's, ...; cmapB[r][k] =
-// (first, end) of A(:,k)'s panel-r run in the copy.  Column-major, a column's
-// ~16 rows (scale 22) share one 64-byte line, so a pass over one panel touches
-// every column's line: all of irA (256 MB) per panel.  Blocked, a panel's runs
-// are contiguous (16 MB).  Panel groups keep the column-major rows.
-__global__ void k_pb_counts(int64_t N, const int2* __restrict__ cmapP, int32_t* __restrict__ cnt) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < N) cnt[i] = cmapP[i].y - cmapP[i].x;
-}
-__global__ void k_pb_map(int64_t N, const int2* __restrict__ cmapP, const int64_t* __restrict__ off,
-                         int2* __restrict__ cmapB) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < N) cmapB[i] = make_int2((int)off[i], (int)off[i] + (cmapP[i].y - cmapP[i].x));
-}
-__global__ void k_pb_copy(int64_t nzcA, const int32_t* __restrict__ jcA, int R, int64_t nA1,
-                          const int2* __restrict__ cmapP, const int2* __restrict__ cmapB,
-                          const int32_t* __restrict__ irA, int32_t* __restrict__ irAB) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= nzcA) return;
-  const int64_t k = jcA[i];
-  for (int r = 0; r < R; ++r) {
-    const int2 e = cmapP[r * nA1 + k];
-    const int d = cmapB[r * nA1 + k].x - e.x;
-    for (int q = e.x; q < e.y; ++q) irAB[d + q] = irA[q];
-  }
-}
-
 // symbolic of the big columns, one block per (column, panel group).
 //
 // A pair (column, panel) is counted into a bitmap of the panel's rows with
@@ -700,8 +672,6 @@ struct SymPanelArgs {
   int64_t nA1;
   const int32_t* irA;
   int64_t m;
-  const int2* cmapB;    // panel-blocked map and rows of A for single-panel units (null: cmapP / irA)
-  const int32_t* irAB;
   int32_t* cnt;
   int32_t* cnt_br;
   int4* desc;
@@ -710,8 +680,6 @@ struct SymPanelArgs {
   int gbm_slots;
   int* gbm_next;
   int* gbm_slot;
-  int gbm_min;
-  int pair_bm;  // count a sparse pair's rows in the panel bitmap (ds_or) instead of an LDS hash (CAS)
   // a multi-slab pair's cut positions (offsets into each B entry's run at every
   // inner slab boundary) for the numeric: cuts[pcoff[br] + (s - 1) * nb + j]
   int* cuts;
@@ -806,13 +774,13 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int R = a.R, plog = a.plog;
   const int64_t* __restrict__ cpB = a.cpB;
   const int32_t* __restrict__ irB = a.irB;
-  const int32_t* __restrict__ irA = a.cmapB ? a.irAB : a.irA;
+  const int32_t* __restrict__ irA = a.irA;
   int32_t* __restrict__ cnt = a.cnt;
   int32_t* __restrict__ cnt_br = a.cnt_br;
   int4* __restrict__ desc = a.desc;
   int32_t* __restrict__ nslab = a.nslab;
   unsigned* __restrict__ gbm = a.gbm;
-  const int gbm_slots = a.gbm_slots, gbm_min = a.gbm_min;
+  const int gbm_slots = a.gbm_slots;
   int* __restrict__ gbm_next = a.gbm_next;
   int* __restrict__ gbm_slot = a.gbm_slot;
   const int pwords = 1 << (plog - 5);
@@ -827,10 +795,9 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int R0 = r << plog;
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), a.m);
   const int words = (R1 - R0 + 31) >> 5;
-  const int2* cm = (a.cmapB ? a.cmapB : a.cmapP) + (int64_t)r * a.nA1;
+  const int2* cm = a.cmapP + (int64_t)r * a.nA1;
   unsigned long long tmark = wall_clock64();
   const int64_t p0 = pre.ok ? pre.p0 : cpB[col], p1 = pre.ok ? pre.p1 : cpB[col + 1];
-  int64_t prod = 0;  // products of the pair
   if (p1 - p0 <= BS) {
     // single chunk: stage once; a pair with few products is counted with an
     // LDS hash sized to it and becomes ONE sparse (hash) slab -- its cost then
@@ -850,15 +817,15 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
     st[tid] = seg_stage(s, ex);
-    prod = total;
     hook(1);
     phase_mark(tmark, 8);
     int T = 512;
     while (T * CBG_PAIR_LOAD_DEN < CBG_PAIR_LOAD_NUM * total) T <<= 1;
-    if (total <= SPARSE_SLAB_MAX && T <= pwords && a.pair_bm) {
+    if (total <= SPARSE_SLAB_MAX && T <= pwords) {
       // the count of a sparse pair from the panel bitmap: one ds_or per product
       // (no returning CAS, no probes), a popcount of the panel's words; the
-      // zeroing is the hash table's for pairs of 2048-4096 products (32 KiB)
+      // zeroing is the hash table's for pairs of 2048-4096 products (32 KiB).
+      // (An LDS hash with bounded probes, before round 5: 0.8 % slower at 22.)
       for (int j = tid; j < pwords / 4; j += BS) reinterpret_cast<uint4*>(bm)[j] = make_uint4(0u, 0u, 0u, 0u);
       if (tid == 0) fine[0] = 0;
       __syncthreads();
@@ -875,56 +842,6 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
           const uint4 x = reinterpret_cast<const uint4*>(bm)[j];
           count += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);  // (words past the panel's end are zero)
         }
-      count = wave_sum(count);
-      if (lane_id() == 0 && count) atomicAdd(&fine[0], count);
-      __syncthreads();
-      if (tid == 0) {
-        const int cnt_pair = fine[0];
-        nslab[br] = cnt_pair ? 1 : 0;
-        if (cnt_pair) desc[(int64_t)br * NFINE_MAX] = make_int4(R0, R1, 0, cnt_pair | SLAB_SPARSE);
-        cnt_br[br] = cnt_pair;
-        if (gbm_slot) gbm_slot[br] = -1;
-        if (cnt_pair) atomicAdd(&cnt[col], cnt_pair);
-      }
-      phase_mark(tmark, 9);
-      return;
-    }
-    if (total <= SPARSE_SLAB_MAX && T <= pwords) {
-      if (c_dbg & 256) {
-        __syncthreads();
-        if (tid == 0) {
-          nslab[br] = 0;
-          cnt_br[br] = 0;
-          if (gbm_slot) gbm_slot[br] = -1;
-        }
-        return;
-      }
-      int* keys = reinterpret_cast<int*>(bm);
-      int* ocount = tmp + BS / WAVE + 3;
-      for (int j = tid; j < T / 4; j += BS)
-        reinterpret_cast<int4*>(keys)[j] = make_int4(EMPTY_KEY, EMPTY_KEY, EMPTY_KEY, EMPTY_KEY);
-      if (tid == 0) *ocount = 0;
-      __syncthreads();
-      int count = 0;
-      const unsigned mask = (unsigned)(T - 1);
-      if (!(c_dbg & 64))
-      block_products<BS>(
-          pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
-          [&](const SegI& g, int u) { return irA[g.off + u]; },
-          [&](int row) {
-            const unsigned h = ((unsigned)row * 0x9E3779B1u) & mask;
-            if (CBG_SYM_OVF > 0)
-              count += hash_claim_bounded<CBG_SYM_OVF>(keys, h, mask, row, ocount, L.ovf, SYM_OVF_CAP);
-            else
-              count += hash_claim(keys, h, mask, row);
-          });
-      hook(2);
-      if (tid == 0) fine[0] = 0;
-      __syncthreads();
-      if (CBG_SYM_OVF > 0) {
-        const int no = *ocount;
-        if (no > 0) count += hash_claim_drain<CBG_SYM_OVF>(keys, mask, L.ovf, min(no, SYM_OVF_CAP));
-      }
       count = wave_sum(count);
       if (lane_id() == 0 && count) atomicAdd(&fine[0], count);
       __syncthreads();
@@ -963,7 +880,6 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
     const int ex = block_excl_scan<BS>(len, tmp, &total);
     pref[tid] = ex;
     if (tid == BS - 1) pref[BS] = total;
-    prod += total;
     st[tid] = seg_stage(s, ex);
     hook(1);
     __syncthreads();
@@ -981,12 +897,12 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   // fine range (2^(FINE_LOG-5) >= 64 words)
   static_assert(FINE_LOG - 5 >= 6, "fine range must hold a wave's words");
   // keep this pair's bitmap for the numeric phase while bitmap slots last
-  // (only for pairs with many products: re-marking a sparse pair in the
-  // numeric phase reads less than storing and reloading its bitmap)
+  // (every bitmap-mode pair: re-marking the ones of 8 K-32 K products in the
+  // numeric instead measured 3-5 % slower, rounds 2 and 5)
   unsigned* gdst = nullptr;
   if (gbm) {
     if (tid == 0) {
-      int slot = prod >= gbm_min ? atomicAdd(gbm_next, 1) : -1;
+      int slot = atomicAdd(gbm_next, 1);
       if (slot >= gbm_slots) slot = -1;
       gbm_slot[br] = slot;
       tmp[0] = slot;
@@ -1256,7 +1172,7 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
       nxt.s = nxt.len = 0;
       nxt.ok = n_p1 - n_p0 <= BS ? 2 : 1;
       if (n_k >= 0) {
-        const int2 e0 = (a.cmapB && n_r1 == n_r0 ? a.cmapB : a.cmapP)[(int64_t)n_r0 * a.nA1 + n_k];
+        const int2 e0 = a.cmapP[(int64_t)n_r0 * a.nA1 + n_k];
         const int e1y = n_r1 > n_r0 ? a.cmapP[(int64_t)n_r1 * a.nA1 + n_k].y : e0.y;
         nxt.s = e0.x;
         nxt.len = e1y - e0.x;
@@ -3040,12 +2956,6 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
   df.take(queue);
 }
 
-// CBG_CUTS=0: the numeric bitmap slabs of multi-slab pairs search their cuts
-// (before round 5) instead of reading the symbolic's
-static bool cuts_enabled() {
-  static const char* e = getenv("CBG_CUTS");
-  return !(e && !strcmp(e, "0"));
-}
 // hash-mode single-panel slabs of more than this many nonzeros run as rank
 // slabs (CBG_RANK_MIN overrides; < 0: none)
 static int rank_slabs_min() {
@@ -3085,19 +2995,6 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
 
 }
 
-// (column, panel) pairs with fewer products re-mark their bitmap in the numeric
-// phase instead of storing it (CBG_GBM_MIN overrides)
-static int gbm_min_products() {
-  static const char* e = getenv("CBG_GBM_MIN");
-  return e ? atoi(e) : 0;
-}
-
-// sparse (column, panel) pairs counted in the panel bitmap (CBG_SYM_PAIR_BM=0:
-// by the LDS hash, before round 5)
-static int sym_pair_bitmap() {
-  static const char* e = getenv("CBG_SYM_PAIR_BM");
-  return !(e && !strcmp(e, "0"));
-}
 
 // kept symbolic bitmaps (32 KiB per (column, panel) pair): CBG_BITMAP_BUDGET_GB,
 // default 48 GB (scale 22 on one GPU: 16 GB -> 32 GB was +3.7 %), never more
@@ -3262,8 +3159,6 @@ struct APrep {
   int plog = -1;
   DBuf<float> valf;  // A's values as f32 (af == 1)
   DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
-  DBuf<int2> cmapB;     // panel-blocked rows of A (CBG_APB): built with cmapP
-  DBuf<int32_t> irAB;
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
 
@@ -3325,11 +3220,6 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned cha
   df.take(c_lo);
 }
 
-// CBG_APB=1: a panel-blocked copy of A's rows for the symbolic's single-panel units
-static bool apb_enabled() {
-  static const char* e = getenv("CBG_APB");
-  return e && !strcmp(e, "1");
-}
 // CBG_APACK=0: the slab kernels read A's rows and f32 values from two arrays
 static bool apack_enabled() {
   static const char* e = getenv("CBG_APACK");
@@ -3351,8 +3241,6 @@ void aprep_end() {
   a.cmapP.release();
   a.valf.release();
   a.valp.release();
-  a.cmapB.release();
-  a.irAB.release();
   a.af = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
@@ -3451,8 +3339,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.cmapP.release();
     ap.valf.release();
     ap.valp.release();
-    ap.cmapB.release();
-    ap.irAB.release();
     ap.af = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
@@ -3656,7 +3542,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
     constexpr int pm_entries = 64;  // map only the referenced A columns when big-column entries * 64 < A's columns
-    bool pmap_full = true;  // cmapP maps every column of A (not only the referenced ones)
     if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
       bp.cmapP = ap.cmapP.p;
     } else if (bp.R > 1 && pm_entries > 0 && big_entries * pm_entries < A.nzc) {
@@ -3669,14 +3554,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       hipLaunchKernelGGL(k_colmap_panels_entries, dim3(nblk((int64_t)nbig * WAVE, 256)), dim3(256), 0, s,
                          bp.perm_big, nbig, B.cp, B.ir, cmap.p, A.ir, bp.plog, bp.R, A.n + 1, bp.cmapP_own.p);
       bp.cmapP = bp.cmapP_own.p;
-      pmap_full = false;
     } else {
       DBuf<int2>& cp = ap.active ? ap.cmapP : bp.cmapP_own;
       cp.reset((size_t)bp.R * (A.n + 1));
-      if (ap.active) {  // a blocked copy made from the previous map is stale
-        ap.cmapB.release();
-        ap.irAB.release();
-      }
       if (bp.R == 1) {
         hipLaunchKernelGGL(k_colmap_panel1, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, cp.p);
       } else {
@@ -3686,35 +3566,6 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       }
       if (ap.active) ap.plog = bp.plog;
       bp.cmapP = cp.p;
-    }
-    // panel-blocked rows of A for the symbolic (CBG_APB), cached like cmapP
-    const int2* cmapB = nullptr;
-    const int32_t* irAB = nullptr;
-    DBuf<int2> cmapB_own;
-    DBuf<int32_t> irAB_own;
-    if (apb_enabled() && bp.R > 1 && pmap_full) {
-      DBuf<int2>& cB = ap.active ? ap.cmapB : cmapB_own;
-      DBuf<int32_t>& iB = ap.active ? ap.irAB : irAB_own;
-      if (!(ap.active && cB.p)) {
-        const int64_t N = (int64_t)bp.R * (A.n + 1);
-        DBuf<int32_t> cnt_pb(N);
-        DBuf<int64_t> off_pb(N + 1);
-        cB.reset(N);
-        iB.reset(std::max<int64_t>(A.nnz, 1));
-        hipLaunchKernelGGL(k_pb_counts, dim3(nblk(N, 256)), dim3(256), 0, s, N, bp.cmapP, cnt_pb.p);
-        exclusive_scan_i32_to_i64(cnt_pb.p, off_pb.p, N, s, &df);
-        hipLaunchKernelGGL(k_pb_map, dim3(nblk(N, 256)), dim3(256), 0, s, N, bp.cmapP, off_pb.p, cB.p);
-        hipLaunchKernelGGL(k_pb_copy, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.jc, bp.R, A.n + 1, bp.cmapP,
-                           cB.p, A.ir, iB.p);
-        df.take(cnt_pb);
-        df.take(off_pb);
-      }
-      cmapB = cB.p;
-      irAB = iB.p;
-      if (!ap.active) {  // this call's own copy: released after the multiply
-        df.take(cmapB_own);
-        df.take(irAB_own);
-      }
     }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
     bp.nslab.reset(nbr);
@@ -3736,7 +3587,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     // a budget (pairs past it leave their cuts to the numeric's searches)
     DBuf<unsigned long long> cuts_next;
     long long cuts_cap = 0;
-    if (!sym_only && cuts_enabled()) {
+    if (!sym_only) {
       cuts_cap = std::min<long long>(INT32_MAX, (long long)(std::min(1.5e9, 0.02 * device_bytes_available()) / 4));
       bp.cuts.reset(std::max<long long>(cuts_cap, 1));
       bp.pcoff.reset(nbr);
@@ -3751,9 +3602,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     };
     set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
-                    cmapB, irAB,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
-                    bp.gbm_slot.p, gbm_min_products(), sym_pair_bitmap(),
+                    bp.gbm_slot.p,
                     bp.cuts.p, cuts_next.p, cuts_cap,
                     bp.pcoff.p};
     // one launch per group class (largest groups first)
