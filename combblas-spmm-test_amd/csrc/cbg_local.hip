@@ -40,7 +40,7 @@ __device__ unsigned long long g_phase[24];
 //   32: k_num_slab counts into g_stat: slabs, non-full slabs, B entries, B entries of non-full slabs, products, nout
 //   64: k_sym_panel skips the hash-count products of sparse pairs and panel groups
 //  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
-//  256: k_sym_panel leaves a hash-mode pair or panel group right after its staging
+//  256: k_sym_panel leaves a panel group right after its staging
 //  512: k_num_slab_hash skips its products       1024: k_num_slab_hash skips its emit
 __device__ unsigned long long g_stat[12];  // [4] bitmap slab products, [7] panel hash, [8] column hash products, [9] hash nnz
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
@@ -1121,6 +1121,9 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
 #else
 #define CBG_SYM_WPE_ATTR
 #endif
+// GROUPS: the launch's units span several panels (sym_group); false for the
+// single-panel class, whose kernel then carries no group code (fewer spills)
+template <bool GROUPS>
 __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelArgs a) {
   // Persistent blocks stride over the units (group-major order kept); the
   // next unit's dependent loads -- column id, B column range, B rows, A run
@@ -1189,7 +1192,7 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
     const int next = unit + (int)gridDim.x;
     start(next);
     bool done = false;
-    if (r1 > r0) done = sym_group(a, L, b, col, r0, r1, cur, hook);
+    if (GROUPS && r1 > r0) done = sym_group(a, L, b, col, r0, r1, cur, hook);
     if (!done) {
       SymPre pp = cur;  // a group run by panels: the column range only
       if (r1 > r0) pp.ok = pp.ok ? 1 : 0;
@@ -3600,7 +3603,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       return (size_t)hw * 4 + NFINE_MAX * 4 + (BIG_BS + 4) * 4 + BIG_BS * 4 + (BIG_BS / WAVE + 4) * 4 +
              (size_t)SYM_OVF_CAP * 4;
     };
-    set_lds(k_sym_panel, lds_of(std::max(pwords, GROUP_T)));
+    set_lds(k_sym_panel<true>, lds_of(std::max(pwords, GROUP_T)));
+    set_lds(k_sym_panel<false>, lds_of(std::max(pwords, GROUP_T)));
     SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p,
@@ -3617,12 +3621,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       sa.ncls = nc;
       static int per_cu = 0;  // resident blocks per CU at the largest LDS size
       if (!per_cu) {
-        CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_sym_panel, BIG_BS,
+        CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_sym_panel<true>, BIG_BS,
                                                              lds_of(std::max(pwords, GROUP_T))));
         if (per_cu < 1) per_cu = 1;
       }
       const int64_t grid = std::min<int64_t>(RG * nc, (int64_t)per_cu * device_cus() * CBG_SYM_WAVES_OF_UNITS);
-      hipLaunchKernelGGL(k_sym_panel, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+      if (sa.glog > 0)
+        hipLaunchKernelGGL(k_sym_panel<true>, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+      else
+        hipLaunchKernelGGL(k_sym_panel<false>, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
     }
   }
   // the thin columns' sort after the big columns' launches (its host
