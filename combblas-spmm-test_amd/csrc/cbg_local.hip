@@ -42,7 +42,8 @@ __device__ unsigned long long g_phase[24];
 //  128: k_sym_panel does not store the kept bitmaps (their slots are still handed out)
 //  256: k_sym_panel leaves a panel group right after its staging
 //  512: k_num_slab_hash skips its products       1024: k_num_slab_hash skips its emit
-__device__ unsigned long long g_stat[12];  // [4] bitmap slab products, [7] panel hash, [8] column hash products, [9] hash nnz
+__device__ unsigned long long g_stat[16];  // [4] bitmap slab products, [7] panel hash, [8] column hash products, [9] hash nnz,
+                                          // [12..15] symbolic groups: counted, their products, run by panels, their products
 __device__ __forceinline__ void phase_mark(unsigned long long& t, int k) {
   if ((c_dbg & 16) && threadIdx.x == 0) {
     const unsigned long long n = wall_clock64();
@@ -686,6 +687,10 @@ struct SymPanelArgs {
   unsigned long long* cuts_next;
   long long cuts_cap;
   int* pcoff;  // per (column, panel) pair, -1: none (pre-set)
+  // group units whose products or nonzeros overflow one hash slab (rare: a few
+  // per phase at scale 22 / 24), run by panels in k_sym_deferred: (b, col, r0, r1)
+  int4* defer;
+  int* defer_n;
 };
 
 // staging of a unit fetched ahead: ok = 1: p0/p1 of the column; ok = 2: also
@@ -1044,6 +1049,10 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   int T = 512;
   while (T * CBG_SYM_LOAD_DEN < CBG_SYM_LOAD_NUM * total) T <<= 1;
   if (T > a.hwords) {
+    if ((c_dbg & 32) && tid == 0) {
+      atomicAdd(&g_stat[14], 1ull);
+      atomicAdd(&g_stat[15], (unsigned long long)total);
+    }
     __syncthreads();
     return false;
   }
@@ -1093,6 +1102,11 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   __syncthreads();
   const int cg = L.fine[0];
   __syncthreads();
+  if ((c_dbg & 32) && tid == 0) {
+    const bool ok = cg <= SPARSE_NNZ_MAX;
+    atomicAdd(&g_stat[ok ? 12 : 14], 1ull);
+    atomicAdd(&g_stat[ok ? 13 : 15], (unsigned long long)total);
+  }
   if (cg > SPARSE_NNZ_MAX) return false;
   if (tid <= r1 - r0) {
     const int64_t br = (int64_t)b * a.R + r0 + tid;
@@ -1121,6 +1135,16 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
 #else
 #define CBG_SYM_WPE_ATTR
 #endif
+__device__ __forceinline__ SymPanelLds sym_lds(char* smem, int hwords) {
+  SymPanelLds L;
+  L.bm = reinterpret_cast<unsigned*>(smem);
+  L.fine = reinterpret_cast<int*>(L.bm + hwords);
+  L.pref = L.fine + NFINE_MAX;
+  L.st = L.pref + BIG_BS + 4;
+  L.tmp = L.st + BIG_BS;
+  L.ovf = L.tmp + BIG_BS / WAVE + 4;
+  return L;
+}
 // GROUPS: the launch's units span several panels (sym_group); false for the
 // single-panel class, whose kernel then carries no group code (fewer spills)
 template <bool GROUPS>
@@ -1132,13 +1156,7 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
   // the start of every block.
   constexpr int BS = BIG_BS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  SymPanelLds L;
-  L.bm = reinterpret_cast<unsigned*>(smem);
-  L.fine = reinterpret_cast<int*>(L.bm + a.hwords);
-  L.pref = L.fine + NFINE_MAX;
-  L.st = L.pref + BS + 4;
-  L.tmp = L.st + BS;
-  L.ovf = L.tmp + BS / WAVE + 4;
+  const SymPanelLds L = sym_lds(smem, a.hwords);
   const int tid = threadIdx.x;
   const int g = 1 << a.glog;
   const int RG = (a.R + g - 1) >> a.glog;
@@ -1191,19 +1209,33 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
     const int b = n_b, col = n_col, r0 = n_r0, r1 = n_r1;
     const int next = unit + (int)gridDim.x;
     start(next);
-    bool done = false;
-    if (GROUPS && r1 > r0) done = sym_group(a, L, b, col, r0, r1, cur, hook);
-    if (!done) {
-      SymPre pp = cur;  // a group run by panels: the column range only
-      if (r1 > r0) pp.ok = pp.ok ? 1 : 0;
-      for (int r = r0; r <= r1; ++r) {
-        sym_pair(a, L, b, col, r, pp, hook);
-        if (r < r1) __syncthreads();  // LDS is reused by the next panel
-      }
+    if constexpr (GROUPS) {
+      // (the panel-by-panel fallback lives in k_sym_deferred, so this kernel
+      // carries only the group hash: no VGPR spills at its 64-VGPR cap)
+      const bool done = r1 > r0 && sym_group(a, L, b, col, r0, r1, cur, hook);
+      if (!done && tid == 0) a.defer[atomicAdd(a.defer_n, 1)] = make_int4(b, col, r0, r1);
+    } else {
+      sym_pair(a, L, b, col, r0, cur, hook);  // (single-panel units: r1 == r0)
     }
     hook(3);
     __syncthreads();  // LDS is reused by the next unit
     unit = next;
+  }
+}
+
+// the deferred group units, panel by panel (their pairs as in k_sym_panel<false>)
+__global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_deferred(SymPanelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SymPanelLds L = sym_lds(smem, a.hwords);
+  const int n = *a.defer_n;
+  auto hook = [](int) {};
+  for (int e = blockIdx.x; e < n; e += gridDim.x) {
+    const int4 d = a.defer[e];
+    const SymPre pp;  // (ok = 0: the pair loads its column range itself)
+    for (int r = d.z; r <= d.w; ++r) {
+      sym_pair(a, L, d.x, d.y, r, pp, hook);
+      __syncthreads();  // LDS is reused by the next panel
+    }
   }
 }
 
@@ -3609,7 +3641,21 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p,
                     bp.cuts.p, cuts_next.p, cuts_cap,
-                    bp.pcoff.p};
+                    bp.pcoff.p, nullptr, nullptr};
+    // group units that overflow one hash slab, collected for k_sym_deferred
+    int64_t group_units = 0;
+    for (int c = 0; c < NGCLS; ++c)
+      if (GROUP_LOG_MAX - c > 0)
+        group_units += (int64_t)sb.count[NSMALL + c] * ((bp.R + (1 << (GROUP_LOG_MAX - c)) - 1) >> (GROUP_LOG_MAX - c));
+    DBuf<int4> defer;
+    DBuf<int> defer_n;
+    if (group_units > 0) {
+      defer.reset(group_units);
+      defer_n.reset(1);
+      CBG_HIP(hipMemsetAsync(defer_n.p, 0, sizeof(int), s));
+      sa.defer = defer.p;
+      sa.defer_n = defer_n.p;
+    }
     // one launch per group class (largest groups first)
     for (int c = 0; c < NGCLS; ++c) {
       const int nc = sb.count[NSMALL + c];
@@ -3630,6 +3676,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
         hipLaunchKernelGGL(k_sym_panel<true>, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
       else
         hipLaunchKernelGGL(k_sym_panel<false>, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+    }
+    if (group_units > 0) {
+      sa.hwords = std::max(pwords, GROUP_T);
+      set_lds(k_sym_deferred, lds_of(sa.hwords));
+      hipLaunchKernelGGL(k_sym_deferred, dim3((unsigned)std::min<int64_t>(group_units, device_cus() * 4)),
+                         dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+      df.take(defer);
+      df.take(defer_n);
     }
   }
   // the thin columns' sort after the big columns' launches (its host
@@ -3847,11 +3901,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16) {
       if (dbg & 32) {
-        unsigned long long gs[12];
+        unsigned long long gs[16];
         CBG_HIP(hipMemcpyFromSymbol(gs, HIP_SYMBOL(g_stat), sizeof(gs)));
         std::fprintf(stderr, "[cbg k_num_slab] slabs %llu nonfull %llu nb %llu nb_nonfull %llu nout %llu multichunk %llu "
-                     "products %llu | hash products panel %llu column %llu nout %llu | rank products %llu nout %llu\n",
-                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6], gs[4], gs[7], gs[8], gs[9], gs[10], gs[11]);
+                     "products %llu | hash products panel %llu column %llu nout %llu | rank products %llu nout %llu"
+                     " | symbolic groups %llu products %llu, by panels %llu products %llu\n",
+                     gs[0], gs[1], gs[2], gs[3], gs[5], gs[6], gs[4], gs[7], gs[8], gs[9], gs[10], gs[11], gs[12], gs[13],
+                     gs[14], gs[15]);
         std::memset(gs, 0, sizeof(gs));
         CBG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stat), gs, sizeof(gs)));
       }
