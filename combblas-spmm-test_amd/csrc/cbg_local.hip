@@ -3685,6 +3685,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       df.take(defer);
       df.take(defer_n);
     }
+    // the symbolic kernels may still run: the counters stay allocated until the
+    // multiply's last synchronization
+    df.take(gbm_next);
+    df.take(cuts_next);
   }
   // the thin columns' sort after the big columns' launches (its host
   // synchronizations would otherwise hold them back)
