@@ -1945,7 +1945,10 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
   }
 }
 
-template <int SR, int CAP, int BS, typename VA>
+// KEPT: every slab of the launch has its kept symbolic bitmap (the host saw
+// that no bitmap-mode pair went without a slot), so the kernel carries no
+// marking pass: 397.5-397.9 vs 403.0-404.4 ms at scale 22 (same box)
+template <int SR, int CAP, int BS, typename VA, bool KEPT>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, const int2* __restrict__ cmapP,
@@ -2019,7 +2022,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     const int lo = rec.lo, hi = rec.hi;
     const int words = rec_words(rec);
     const int64_t obase = rec.obase;
-    const bool have_bm = rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
+    const bool have_bm = KEPT || rec.slot >= 0;  // bitmap kept by the symbolic phase: no marking pass
     const bool pre = staged(rec);        // chunk 0 staging came in registers
     if ((c_dbg & 32) && tid == 0) {
       atomicAdd(&g_stat[0], 1ull);
@@ -2058,7 +2061,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (has_next) nrec = list[inext];
     phase_mark(tmark, 0);
     const int64_t p0 = rec.p0, p1 = rec.p0 + rec.nb;
-    const int first_pass = have_bm ? 1 : 0;
+    const int first_pass = KEPT ? 1 : have_bm ? 1 : 0;
     for (int pass = first_pass; pass < 2; ++pass) {
       if (pass == 1) {
         // ranks: exclusive prefix of popcounts over the slab's words; thread t
@@ -2916,6 +2919,9 @@ struct BigPlan {
   const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
   const PackedRV* valAp = nullptr;  // ... and as (row, f32) records (CBG_APACK)
   DBuf<int> cuts, pcoff;  // multi-slab pairs' cut positions (sym_pair), per-pair offsets
+  const int* gbm_next = nullptr;  // kept-bitmap slots handed out (device), of gbm_slots
+  int64_t gbm_slots = 0;
+  bool all_kept = false;  // no bitmap-mode pair went without a slot (read with sync 3)
 };
 
 
@@ -2960,10 +2966,17 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
                        A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p, bp.cuts.p);
   };
-  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
-  if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV>, bp.valAp, per_cu_p);
-  else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float>, bp.valAf, per_cu_f);
-  else go(k_num_slab<SR, CAP, BS, double>, A.val, per_cu_d);
+  static int per_cu_d[2] = {}, per_cu_f[2] = {}, per_cu_p[2] = {};
+  const int kk = bp.all_kept ? 1 : 0;
+  if (bp.all_kept) {
+    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true>, bp.valAp, per_cu_p[kk]);
+    else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float, true>, bp.valAf, per_cu_f[kk]);
+    else go(k_num_slab<SR, CAP, BS, double, true>, A.val, per_cu_d[kk]);
+  } else {
+    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false>, bp.valAp, per_cu_p[kk]);
+    else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float, false>, bp.valAf, per_cu_f[kk]);
+    else go(k_num_slab<SR, CAP, BS, double, false>, A.val, per_cu_d[kk]);
+  }
   df.take(queue);
 }
 
@@ -3687,6 +3700,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     }
     // the symbolic kernels may still run: the counters stay allocated until the
     // multiply's last synchronization
+    bp.gbm_next = gbm_next.p;
+    bp.gbm_slots = nslots;
     df.take(gbm_next);
     df.take(cuts_next);
   }
@@ -3812,8 +3827,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        bp.gbm_slot.p, bp.plog, A.m, bp.pcoff.p);
     int* ncls_h = reinterpret_cast<int*>(host_stage(STAGE_SLABS));
     CBG_HIP(hipMemcpyAsync(ncls_h, counters.p + 2 * NK, SLAB_NCLS * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (bp.gbm_next)
+      CBG_HIP(hipMemcpyAsync(ncls_h + SLAB_NCLS, bp.gbm_next, sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));  // host sync 3 of 4: the slab classes' sizes
     std::memcpy(ncls, ncls_h, sizeof(int) * SLAB_NCLS);
+    bp.all_kept = bp.gbm_next && (int64_t)ncls_h[SLAB_NCLS] <= bp.gbm_slots;
     df.take(counters);
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
