@@ -51,7 +51,6 @@ def load_cbg():
 # (broadcast piece by piece behind the multiply); measured per rank tile on one
 # GPU: 2x1 7 % and 4x2 2-13 % faster than 1x2 / 2x4.  --grid RxC overrides.
 GRIDS = {1: (1, 1), 2: (2, 1), 4: (2, 2), 8: (4, 2), 9: (3, 3), 16: (4, 4)}
-ROUND = "r05"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -108,21 +107,37 @@ def host_cores():
     return max(cores, 1), dict(affinity=n, cgroup_quota=quota, **shape)
 
 
+def newest_profile(suffix, accept=lambda d: True, root=None):
+    """The newest committed record profiles/rNN_<suffix> (highest round NN) whose
+    JSON `accept` takes, as (dict, path relative to the repo), or (None, None)."""
+    import re
+    root = root or os.path.join(REPO, "profiles")
+    pat = re.compile(r"^r(\d+)_" + re.escape(suffix) + "$")
+    found = []
+    for name in os.listdir(root) if os.path.isdir(root) else []:
+        m = pat.match(name)
+        if m:
+            found.append((int(m.group(1)), name))
+    for _, name in sorted(found, reverse=True):
+        path = os.path.join(root, name)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if accept(d):
+            return d, os.path.relpath(path, REPO)
+    return None, None
+
+
 def pmc_traffic(scale, ef, phases):
     """HBM bytes of one local multiply (all phases) at this configuration from the
-    committed PMC passes (profiles/<round>_traffic_s<scale>.json, made by
+    newest committed PMC passes (profiles/rNN_traffic_s<scale>.json, made by
     tools/profile_round.sh + tools/traffic.py: FETCH_SIZE calibrated on k_digest,
-    + WRITE_SIZE), this round's file first, or None."""
-    for rnd in (ROUND, "r03", "r02", "r01"):
-        path = os.path.join(REPO, "profiles", "%s_traffic_s%d.json" % (rnd, scale))
-        if not os.path.exists(path):
-            continue
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("scale") != scale or d.get("ef") != ef or d.get("phases", 1) != phases:
-            continue
-        return d["traffic_bytes"], os.path.relpath(path, REPO)
-    return None, None
+    + WRITE_SIZE), or None."""
+    d, path = newest_profile("traffic_s%d.json" % scale, lambda d: d.get("scale") == scale and d.get("ef") == ef
+                             and d.get("phases", 1) == phases)
+    return (d["traffic_bytes"], path) if d else (None, None)
 
 
 REF_DRIVER = os.path.join(REPO, "oracle", "_ref", "ref_driver")
@@ -171,16 +186,12 @@ def cpu_baseline_reference(scale, ef, threads, algos=("synch",)):
 
 
 def cpu_baseline_s22():
-    """The one-off reference run at the metric's own scale (profiles/<round>_cpu_reference_s22.json,
+    """The newest reference run at the metric's own scale (profiles/rNN_cpu_reference_s22.json,
     tools/cpu_reference_s22.sh on the GPU box: Mult_AnXBn_Synch per B-column phase)."""
-    for rnd in (ROUND, "r03", "r02", "r01"):
-        path = os.path.join(REPO, "profiles", "%s_cpu_reference_s22.json" % rnd)
-        if os.path.exists(path):
-            with open(path) as f:
-                d = json.load(f)
-            d["source"] = os.path.relpath(path, REPO)
-            return d
-    return None
+    d, path = newest_profile("cpu_reference_s22.json", lambda d: "value" in d)
+    if d is not None:
+        d["source"] = path
+    return d
 
 
 def cpu_baseline(scale, ef, seed, threads):
@@ -502,6 +513,13 @@ def main():
             out["roofline"]["frac_f64_values"] = f64["frac"]
             out["f64_values"] = f64
         if N == 1 and not a.no_cpu_baseline:
+            # the reference at the metric's own scale (a committed run on the GPU box's
+            # host, ~6 min) first; cpu_baseline below is the bounded live sample
+            s22 = cpu_baseline_s22()
+            if s22 is not None and scale == 22:
+                s22["scale"] = 22
+                s22["gpu_over_cpu"] = out["value"] / s22["value"]
+                out["cpu_baseline_s22"] = s22
             cores, host = host_cores()
             threads = a.cpu_threads or cores
             cs = a.cpu_scale
@@ -509,7 +527,7 @@ def main():
             if ref is not None:
                 r, algo_, cdt, cnnz = ref
                 out["cpu_baseline"] = {"value": r, "unit": "nnz(C)/s", "cores": threads, "kind": "reference",
-                                       "sample": "R-MAT scale-%d ef%d A*A, the reference's Mult_AnXBn_%s 1x1 "
+                                       "scale": cs, "sample": "R-MAT scale-%d ef%d A*A, the reference's Mult_AnXBn_%s 1x1 "
                                                  "(oracle/_ref/ref_driver), %.1f s on %d threads" % (
                                                      cs, a.ef, algo_.capitalize(), cdt, threads),
                                        "host": host}
@@ -522,12 +540,8 @@ def main():
             else:
                 r, algo_, cdt, cnnz = cpu_baseline(cs, a.ef, a.seed, threads)
                 out["cpu_baseline"] = {"value": r, "unit": "nnz(C)/s", "cores": threads, "kind": "port",
-                                       "sample": "R-MAT scale-%d ef%d A*A, oracle Mult_AnXBn_%s 1x1, %.1f s" % (
+                                       "scale": cs, "sample": "R-MAT scale-%d ef%d A*A, oracle Mult_AnXBn_%s 1x1, %.1f s" % (
                                            cs, a.ef, algo_.capitalize(), cdt), "host": host}
-            s22 = cpu_baseline_s22()
-            if s22 is not None and scale == 22:
-                out["cpu_baseline_s22"] = s22
-                out["cpu_baseline_s22"]["gpu_over_cpu"] = out["value"] / s22["value"]
         print(json.dumps(out), flush=True)
     if C is not None:
         C.tile.free()

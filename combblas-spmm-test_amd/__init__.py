@@ -76,7 +76,7 @@ EXPORTS = [
     "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
     "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info", "cbg_summa_spgemm_memeff",
     "cbg_last_summa_comm",
-    "cbg_last_phase_plan",
+    "cbg_last_phase_plan", "cbg_last_work_stats",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -121,6 +121,7 @@ def lib():
         "cbg_merge": ([T, i32, i32, T, vp], i32),
         "cbg_last_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
+        "cbg_last_work_stats": ([ctypes.POINTER(i64), i32], i32),
         "cbg_get_unique_id": ([vp], i32),
         "cbg_grid_create": ([i32, i32, i32, i32, vp, ctypes.POINTER(vp)], i32),
         "cbg_grid_create_host": ([i32, i32, i32, i32, ctypes.POINTER(CHostComm), ctypes.POINTER(vp)], i32),
@@ -394,6 +395,25 @@ def last_stats():
                          ctypes.byref(ns))
     return dict(flops=f.value, nnz=n.value, ms_symbolic=a.value, ms_numeric=b.value, n_big=nb.value,
                 n_slabs=ns.value)
+
+
+# cbg_last_work_stats classes (include/cbg.h CBG_WORK_*), in order
+WORK_CLASSES = (["bitmap_small_kept", "bitmap_small_mark", "bitmap_large_kept", "bitmap_large_mark"] +
+                ["hash_T%d" % t for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)] +
+                ["rank_N%d" % n for n in (1024, 2048, 4096)] +
+                ["sym_panel_units", "sym_group_units", "sym_deferred_units", "esc_columns", "thin_columns",
+                 "single_big_entries", "hash_bin_columns", "wave_bin_columns"])
+
+
+def last_work_stats():
+    """the work of each kernel family in the last call's local multiplies (summed):
+    numeric slabs per launch class, symbolic units, small-column passes -- which
+    code paths ran (cbg_last_work_stats)"""
+    buf = (ctypes.c_int64 * len(WORK_CLASSES))()
+    n = lib().cbg_last_work_stats(buf, len(WORK_CLASSES))
+    if n != len(WORK_CLASSES):
+        raise CbgError(-1, "cbg_last_work_stats reports %d classes, the mirror knows %d" % (n, len(WORK_CLASSES)))
+    return dict(zip(WORK_CLASSES, buf))
 
 
 def summa_info():

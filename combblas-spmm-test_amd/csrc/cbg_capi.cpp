@@ -374,6 +374,12 @@ int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_sym, double* ms_num,
   return CBG_OK;
 }
 
+int cbg_last_work_stats(int64_t* counts, int n) {
+  const cbg::LocalStats& g_stats = cbg::thread_stats();
+  for (int i = 0; counts && i < n && i < CBG_WORK_N; ++i) counts[i] = g_stats.work[i];
+  return CBG_WORK_N;
+}
+
 // ---------------- grid ----------------
 int cbg_get_unique_id(void* id);  // cbg_summa_id.cpp
 

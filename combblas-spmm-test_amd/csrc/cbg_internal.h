@@ -54,6 +54,15 @@ class DevicePool {
   // again gets a new one); 0 if p is not in a live pool block
   uint64_t serial_of(const void* p);
   size_t bytes_cached() const { return cached_; }
+  // Debug mode (CBG_POOL_QUARANTINE=1, read once): a freed block is poisoned at
+  // once on a stream of its own (0xff bytes: row ids -1, values NaN), racing any
+  // kernel that may still use it, and is not handed out again before
+  // quarantine_release() (a device synchronization; every local multiply's end),
+  // so a buffer released while a kernel can still read it shows up as a wrong
+  // result, not as a rare race with the block's next owner.
+  bool quarantine() const { return quarantine_; }
+  void quarantine_release();
+  DevicePool();
   ~DevicePool() { trim(); }
 
  private:
@@ -70,6 +79,9 @@ class DevicePool {
   std::map<void*, uint64_t> serial_;      // live blocks (regular and growable) -> allocation serial
   uint64_t next_serial_ = 0;
   size_t in_use_ = 0, cached_ = 0;
+  bool quarantine_ = false;
+  std::vector<std::pair<void*, size_t>> quar_;  // freed, poisoned, not yet reusable
+  hipStream_t poison_ = nullptr;
 };
 DevicePool& pool();
 
@@ -137,6 +149,7 @@ struct DeferredFree {
     // use the buffers, so wait before they can be handed out again
     if (!synced && !ptrs.empty()) (void)hipDeviceSynchronize();
     for (void* q : ptrs) pool().free(q);
+    if (pool().quarantine()) pool().quarantine_release();
   }
 };
 
@@ -146,6 +159,7 @@ struct LocalStats {
   int64_t nnz = 0;
   int64_t n_big = 0, n_slabs = 0;
   double ms_symbolic = 0, ms_numeric = 0;
+  int64_t work[CBG_WORK_N] = {};  // cbg_last_work_stats
 };
 // Every call accumulates into the calling thread's stats (reset by the C ABI
 // at the start of each public entry point); `st` optionally receives this call's.

@@ -23,6 +23,9 @@
 // take consecutive products, so reads of A's columns are coalesced whatever
 // their length (R-MAT hub columns included).
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <cstring>
 #include <type_traits>
 
@@ -580,8 +583,8 @@ constexpr int SPARSE_SLAB_MAX = CBG_SPARSE_SLAB_MAX;  // products of a (column, 
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
 constexpr int SLAB_CNT_MASK = SLAB_SPARSE - 1;
 
-// Panel column maps of A: cmapP[r * (n+1) + k] = (first, end) of column k's
-// entries in row panel r.  A panel without rows of A(:,k) gets (q, q) with q
+// Panel column maps of A: entry (r, k) = (first, end) of column k's entries
+// in row panel r (layout: PMap below).  A panel without rows of A(:,k) gets (q, q) with q
 // the lower bound of the panel's first row, so that (cmapP[r0].x,
 // cmapP[r1].y) is A(:,k)'s run over panels r0..r1 (panel groups); columns
 // absent from A stay (0, 0) (the caller's memset).  One
@@ -589,9 +592,21 @@ constexpr int SLAB_CNT_MASK = SLAB_SPARSE - 1;
 // binary-searches each panel boundary (long ones) and writes its R entries,
 // so every store of a wave is one row of the map at consecutive columns
 // (coalesced; one thread per entry scattering over R rows was 3x slower).
+//
+// Layout: entry (r, k) at r * sr + k * sk.  Panel-major (sr = n + 1, sk = 1)
+// or column-major (sr = 1, sk = R: a column's R entries share one or two
+// lines, read once by the column's R units when they run together on one
+// XCD); the whole-column map of the column bins as a map of one panel (sr = 0,
+// sk = 1).
+struct PMap {
+  const int2* p;
+  int64_t sr;
+  int sk;
+  __device__ __forceinline__ int2 at(int r, int k) const { return p[(int64_t)r * sr + (int64_t)k * sk]; }
+};
 // A(:,k) = rows irA[a, e): its run inside every row panel, one thread
 __device__ __forceinline__ void panel_runs(const int32_t* __restrict__ irA, int a, int e, int plog, int R,
-                                           int64_t nA1, int64_t k, int2* __restrict__ cmapP) {
+                                           int64_t sr, int sk, int64_t k, int2* __restrict__ cmapP) {
   int pos = a;
   for (int r = 0; r < R; ++r) {
     const int lo = pos;
@@ -605,29 +620,29 @@ __device__ __forceinline__ void panel_runs(const int32_t* __restrict__ irA, int 
         pos = lower_bound_g(irA, pos, e, bound);
       }
     }
-    cmapP[r * nA1 + k] = make_int2(lo, pos);
+    cmapP[r * sr + k * sk] = make_int2(lo, pos);
   }
 }
 __global__ void k_colmap_panels_col(int64_t nzcA, const int64_t* __restrict__ cpA, const int32_t* __restrict__ jcA,
-                                    const int32_t* __restrict__ irA, int plog, int R, int64_t nA1,
+                                    const int32_t* __restrict__ irA, int plog, int R, int64_t sr, int sk,
                                     int2* __restrict__ cmapP) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= nzcA) return;
-  panel_runs(irA, (int)cpA[i], (int)cpA[i + 1], plog, R, nA1, jcA[i], cmapP);
+  panel_runs(irA, (int)cpA[i], (int)cpA[i + 1], plog, R, sr, sk, jcA[i], cmapP);
 }
 // the same for the A columns the big B columns reference only (a wave per big
 // column, a lane per entry; a column referenced twice is written twice alike)
 __global__ void k_colmap_panels_entries(const int32_t* __restrict__ perm_big, int nbig,
                                         const int64_t* __restrict__ cpB, const int32_t* __restrict__ irB,
                                         const int2* __restrict__ cmap, const int32_t* __restrict__ irA, int plog,
-                                        int R, int64_t nA1, int2* __restrict__ cmapP) {
+                                        int R, int64_t sr, int sk, int2* __restrict__ cmapP) {
   const int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE;
   if (w >= nbig) return;
   const int col = perm_big[w];
   for (int64_t p = cpB[col] + lane_id(); p < cpB[col + 1]; p += WAVE) {
     const int k = irB[p];
     const int2 e = cmap[k];
-    panel_runs(irA, e.x, e.x + e.y, plog, R, nA1, k, cmapP);
+    panel_runs(irA, e.x, e.x + e.y, plog, R, sr, sk, k, cmapP);
   }
 }
 
@@ -669,8 +684,7 @@ struct SymPanelArgs {
   int ncls;  // columns of this launch class (units = ncls x panel groups)
   const int64_t* cpB;
   const int32_t* irB;
-  const int2* cmapP;
-  int64_t nA1;
+  PMap pm;
   const int32_t* irA;
   int64_t m;
   int32_t* cnt;
@@ -800,7 +814,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   const int R0 = r << plog;
   const int R1 = (int)min((int64_t)R0 + (1LL << plog), a.m);
   const int words = (R1 - R0 + 31) >> 5;
-  const int2* cm = a.cmapP + (int64_t)r * a.nA1;
+  auto cm = [&](int k) { return a.pm.at(r, k); };
   unsigned long long tmark = wall_clock64();
   const int64_t p0 = pre.ok ? pre.p0 : cpB[col], p1 = pre.ok ? pre.p1 : cpB[col + 1];
   if (p1 - p0 <= BS) {
@@ -813,7 +827,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       s = pre.s;
       len = pre.len;
     } else if (p < p1) {
-      const int2 e = cm[irB[p]];
+      const int2 e = cm(irB[p]);
       s = e.x;
       len = e.y - e.x;
     }
@@ -877,7 +891,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
   for (int64_t c0 = p0; c0 < p1; c0 += BS) {    const int64_t p = c0 + tid;
     int s = 0, len = 0;
     if (p < p1) {
-      const int2 e = cm[irB[p]];
+      const int2 e = cm(irB[p]);
       s = e.x;
       len = e.y - e.x;
     }
@@ -1003,7 +1017,7 @@ __device__ __forceinline__ void sym_pair(const SymPanelArgs& a, const SymPanelLd
       const int off = L.ovf[1];
       if (off >= 0)
         for (int64_t j = tid; j < nb; j += BS) {
-          const int2 ce = cm[irB[p0 + j]];
+          const int2 ce = cm(irB[p0 + j]);
           int pos = ce.x;
           for (int q = 1; q < ns; ++q) {
             pos = lower_bound_g(irA, pos, ce.y, L.ovf[1 + q]);
@@ -1028,8 +1042,6 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   const int tid = threadIdx.x;
   const int64_t p0 = pre.ok ? pre.p0 : a.cpB[col], p1 = pre.ok ? pre.p1 : a.cpB[col + 1];
   if (p1 - p0 > BS) return false;
-  const int2* c0 = a.cmapP + (int64_t)r0 * a.nA1;
-  const int2* c1 = a.cmapP + (int64_t)r1 * a.nA1;
   const int64_t p = p0 + tid;
   int s = 0, len = 0;
   if (pre.ok == 2) {
@@ -1037,8 +1049,8 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
     len = pre.len;
   } else if (p < p1) {
     const int k = a.irB[p];
-    s = c0[k].x;
-    len = c1[k].y - s;
+    s = a.pm.at(r0, k).x;
+    len = a.pm.at(r1, k).y - s;
   }
   int total;
   const int ex = block_excl_scan<BS>(len, L.tmp, &total);
@@ -1122,9 +1134,7 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
   return true;
 }
 
-// grid: RG groups x (columns of the class), group-major, so that the blocks in
-// flight gather A's segments of the same panels, which then stay in L2 /
-// Infinity Cache
+// grid: RG groups x (columns of the class) in XCD column order (k_sym_panel)
 #ifndef CBG_SYM_WPE  // waves per SIMD k_sym_panel is compiled for (0: the compiler's choice)
 // 8: at most 64 VGPRs, so 4 blocks of 512 threads per CU (the LDS allows 4; at
 // 65 VGPRs only 3 fit): +4.2 % at scale 22 (profiles/r04_ab_hash_sym.json)
@@ -1161,19 +1171,31 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
   const int g = 1 << a.glog;
   const int RG = (a.R + g - 1) >> a.glog;
   const int ncls = a.ncls;
-  const int nunits = ncls * RG;
   // next unit's fetch state
   int n_b = 0, n_r0 = 0, n_r1 = 0, n_col = 0, n_k = -1, stage = -1;
   int64_t n_p0 = 0, n_p1 = 0;
+  // XCD column order: unit u goes to the blocks b = u (mod 8), which MI355X
+  // places on one XCD (blocks are dealt round-robin over the 8 XCDs, and the
+  // grid is a multiple of 8); they take the columns x, x + 8, ... of the class,
+  // each column's RG units one after the other, so the blocks in flight on an
+  // XCD are a few columns' panels, which read the same B entries, the same
+  // column-major map lines and -- A's short columns -- the same lines of A:
+  // L2 hits 27.6 -> 44.5 % (single panels) and 13.9 -> 40.1 % (groups), the
+  // kernel 87 -> 72.7 ms per scale-22 step (profiles/r06_l2_s22_*.txt).  The
+  // panel-major order before kept every block on one panel, reusing the hub
+  // columns' runs in the Infinity Cache instead.
+  // false: no unit left for this block
   auto start = [&](int unit) {
     stage = -1;
-    if (unit >= nunits) return;
-    const int rg = unit / ncls;
-    n_b = a.boff + unit % ncls;
+    const int x = unit & 7, s = unit >> 3, cq = s / RG;
+    const int ci = x + 8 * cq, rg = s - cq * RG;
+    if (ci >= ncls) return false;
+    n_b = a.boff + ci;
     n_r0 = rg << a.glog;
     n_r1 = min(n_r0 + g, a.R) - 1;
     n_col = a.perm_big[n_b];
     stage = 0;
+    return true;
   };
   SymPre nxt;
   auto hook = [&](int k) {
@@ -1193,8 +1215,8 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
       nxt.s = nxt.len = 0;
       nxt.ok = n_p1 - n_p0 <= BS ? 2 : 1;
       if (n_k >= 0) {
-        const int2 e0 = a.cmapP[(int64_t)n_r0 * a.nA1 + n_k];
-        const int e1y = n_r1 > n_r0 ? a.cmapP[(int64_t)n_r1 * a.nA1 + n_k].y : e0.y;
+        const int2 e0 = a.pm.at(n_r0, n_k);
+        const int e1y = n_r1 > n_r0 ? a.pm.at(n_r1, n_k).y : e0.y;
         nxt.s = e0.x;
         nxt.len = e1y - e0.x;
       }
@@ -1202,13 +1224,13 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
     }
   };
   int unit = blockIdx.x;
-  start(unit);
+  bool valid = start(unit);
   hook(3);
-  while (unit < nunits) {
+  while (valid) {
     const SymPre cur = nxt;
     const int b = n_b, col = n_col, r0 = n_r0, r1 = n_r1;
     const int next = unit + (int)gridDim.x;
-    start(next);
+    const bool nvalid = start(next);
     if constexpr (GROUPS) {
       // (the panel-by-panel fallback lives in k_sym_deferred, so this kernel
       // carries only the group hash: no VGPR spills at its 64-VGPR cap)
@@ -1220,6 +1242,7 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
     hook(3);
     __syncthreads();  // LDS is reused by the next unit
     unit = next;
+    valid = nvalid;
   }
 }
 
@@ -1271,6 +1294,8 @@ __constant__ int c_hash_t[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
 // hash-mode slabs of more than rank_min nonzeros spanning <= rank_span rows
 // (one panel; rank_span 0: none)
 constexpr int SLAB_RANK_NCLS = 3;
+static_assert(CBG_WORK_RANK0 - CBG_WORK_HASH0 == SLAB_HASH_NCLS && CBG_WORK_SYM_PANEL_UNITS - CBG_WORK_RANK0 == SLAB_RANK_NCLS,
+              "cbg_last_work_stats classes");
 constexpr int SLAB_RANK0 = 2 + SLAB_HASH_NCLS;
 constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS + SLAB_RANK_NCLS;
 __device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank_span, int rank_min) {
@@ -1951,8 +1976,8 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
 template <int SR, int CAP, int BS, typename VA, bool KEPT>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
-                                                 const double* __restrict__ valB, const int2* __restrict__ cmapP,
-                                                 int64_t nA1, const int32_t* __restrict__ irA,
+                                                 const double* __restrict__ valB, PMap pm,
+                                                 const int32_t* __restrict__ irA,
                                                  const VA* __restrict__ valA,
                                                  int32_t* __restrict__ out_ir,
                                                  double* __restrict__ out_val, const unsigned* __restrict__ gbm,
@@ -1976,6 +2001,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   static_assert(WPT % 8 == 0 && (CAP * 8 + BS * 8) % 16 == 0, "rank scan vectors");
   const int tid = threadIdx.x;
   const int wslot = 1 << (plog - 5);
+  constexpr int NW = BS / WAVE;
   int i = blockIdx.x;
   if (i >= n) return;
   // prefetch registers (bitmap words in 16-byte lane vectors: words 4 (k*BS + tid) .. +3)
@@ -2008,7 +2034,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
   };
   auto fetch_stage2 = [&](const SlabRec& r) {
-    if (staged(r) && tid < r.nb) p_ce = cmapP[(int64_t)r.r * nA1 + p_ir];
+    if (staged(r) && tid < r.nb) p_ce = pm.at(r.r, p_ir);
   };
   SlabRec rec = list[i];
   fetch_words(rec);
@@ -2016,8 +2042,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
   fetch_stage2(rec);
   while (true) {
     // ---- next work item (its record arrives while this slab fills LDS)
-    if (tid == 0) tmp[BS / WAVE + 2] = (int)gridDim.x + atomicAdd(queue, 1);
-    const int2* cm = cmapP + (int64_t)rec.r * nA1;
+    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
     const int nout = rec.nout;
     const int lo = rec.lo, hi = rec.hi;
     const int words = rec_words(rec);
@@ -2055,7 +2080,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       bv[tid] = tid < rec.nb ? p_bv : 0.0;
     }
     __syncthreads();
-    const int inext = tmp[BS / WAVE + 2];
+    const int inext = tmp[NW + 2];
     const bool has_next = inext < n;
     SlabRec nrec;
     if (has_next) nrec = list[inext];
@@ -2111,7 +2136,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           int s = 0, len = 0;
           double bval = 0.0;
           if (p < p1) {
-            const int2 ce = cm[irB[p]];
+            const int2 ce = pm.at(rec.r, irB[p]);
             if (rec.flags & SLAB_FULL) {
               s = ce.x;
               len = ce.y - ce.x;
@@ -2337,8 +2362,8 @@ struct SlabHashLds {
 template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
 __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
-                                                      const double* __restrict__ valB, const int2* __restrict__ cmapP,
-                                                      int64_t nA1, const int32_t* __restrict__ irA,
+                                                      const double* __restrict__ valB, PMap pm,
+                                                      const int32_t* __restrict__ irA,
                                                       const VA* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir,
                                                       double* __restrict__ out_val) {
@@ -2383,11 +2408,11 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
   // A(:,k)'s run over the slab's rows: one map entry, or the first and last
   // panels' entries of a panel group (rows [lo, hi) span panels r .. r1)
   auto seg_of = [&](const SlabRec& r, int k) -> int2 {
-    const int2 e = cmapP[(int64_t)r.r * nA1 + k];
+    const int2 e = pm.at(r.r, k);
     if (CMLEN) return make_int2(e.x, e.x + e.y);
     const int r1 = (r.hi - 1) >> plog;
     if (r1 == r.r) return e;
-    return make_int2(e.x, cmapP[(int64_t)r1 * nA1 + k].y);
+    return make_int2(e.x, pm.at(r1, k).y);
   };
   auto fetch2 = [&](const SlabRec& r) {
     if (!staged(r)) return;
@@ -2517,6 +2542,9 @@ struct SlabRankLds {
   static_assert(SEG_BYTES % 16 == 0 && BM_OFF % 16 == 0 && GPRE_OFF % 16 == 0, "rank slab LDS alignment");
 };
 constexpr int RANK_BS = 512;
+// a rank slab stages one B entry per thread: the symbolic's sparse pairs (the
+// rank slabs' source, sym_pair) have <= BIG_BS B entries
+static_assert(BIG_BS <= RANK_BS, "rank slabs stage <= RANK_BS B entries");
 static_assert(SPARSE_SLAB_MAX % RANK_BS == 0 && SPARSE_SLAB_MAX / RANK_BS <= 16, "rank slab products per lane");
 static_assert(SPARSE_SLAB_MAX == 8 * RANK_BS, "segment scan: 8 products per thread");
 
@@ -2527,7 +2555,7 @@ template <int SR, int NCAP, int BS, typename VA>
 __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict__ list, int n,
                                                       int* __restrict__ queue, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB,
-                                                      const int2* __restrict__ cmapP, int64_t nA1,
+                                                      PMap pm,
                                                       const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
   using L = SlabRankLds<NCAP, BS>;
@@ -2558,7 +2586,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
     }
   };
   auto fetch2 = [&](const SlabRec& r) {
-    if (tid < r.nb) p_ce = cmapP[(int64_t)r.r * nA1 + p_ir];
+    if (tid < r.nb) p_ce = pm.at(r.r, p_ir);
   };
   SlabRec rec = list[i];
   fetch1(rec);
@@ -2722,14 +2750,40 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                        OutSink* sink, bool sym_only = false);
 static inline unsigned nblk(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// Device properties and occupancy are cached per (device, kernel, block size,
+// LDS bytes): a process may drive several GPUs from several threads (one
+// thread per GPU), and one kernel is launched at several LDS sizes.
+static std::mutex& occ_mutex() {
+  static std::mutex m;
+  return m;
+}
 static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    CBG_HIP(hipGetDevice(&dev));
-    CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  static std::map<int, int> cache;
+  int dev = 0;
+  CBG_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(occ_mutex());
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int cus = 0;
+  CBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  cache[dev] = cus;
   return cus;
+}
+// resident blocks per CU of `kernel` at BS threads and `lds` bytes of LDS (>= 1)
+template <class K>
+static int blocks_per_cu(K kernel, int bs, size_t lds) {
+  static std::map<std::tuple<int, const void*, int, size_t>, int> cache;
+  int dev = 0;
+  CBG_HIP(hipGetDevice(&dev));
+  const auto key = std::make_tuple(dev, (const void*)kernel, bs, lds);
+  std::lock_guard<std::mutex> lk(occ_mutex());
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int n = 0;
+  CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)kernel, bs, lds));
+  n = std::max(n, 1);
+  cache[key] = n;
+  return n;
 }
 
 // CUs the persistent kernels (slab queues) may fill: all of them, less
@@ -2887,22 +2941,18 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
   while ((1LL << lm) < A.m) ++lm;  // emit buckets span [0, 2^lm)
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  auto go = [&](auto k, const auto* valA, int& per_cu) {
+  auto go = [&](auto k, const auto* valA) {
     set_lds(k, L);
-    if (!per_cu) {
-      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-      if (per_cu < 1) per_cu = 1;
-    }
+    const int per_cu = blocks_per_cu(k, BS, L);
     // (a quarter / a 16th of the resident blocks, leaving the big-column slabs on
     // the main stream more CUs: 424 / 537 vs 418.5 ms at scale 22)
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, cmap,
-                       (int64_t)0, A.ir, valA, C.ir, C.val);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, PMap{cmap, 0, 1},
+                       A.ir, valA, C.ir, C.val);
   };
   // A's f32 values (exact, see k_vals_f32) when the big-column path made them
-  static int per_cu_d = 0, per_cu_f = 0;
-  if (valAf) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, float>, valAf, per_cu_f);
-  else go(k_num_slab_hash<SR, 1 << LOGT, BS, true, double>, A.val, per_cu_d);
+  if (valAf) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, float>, valAf);
+  else go(k_num_slab_hash<SR, 1 << LOGT, BS, true, double>, A.val);
   df.take(rec);
   df.take(queue);
 }
@@ -2912,6 +2962,9 @@ struct BigPlan {
   const int32_t* perm_big = nullptr;
   const int2* cmapP = nullptr;  // panel column maps (cached across phases, or cmapP_own)
   DBuf<int2> cmapP_own;
+  bool kmajor = false;  // cmapP column-major (PMap)
+  int64_t n1 = 0;       // A's columns + 1
+  PMap pm() const { return kmajor ? PMap{cmapP, 1, R} : PMap{cmapP, n1, 1}; }
   DBuf<int4> desc;
   DBuf<int32_t> nslab, cnt_br;
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
@@ -2926,90 +2979,71 @@ struct BigPlan {
 
 
 template <int SR, int T, int BS>
-static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                             cbg_tile& C, hipStream_t s, DeferredFree& df) {
+static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
+                             const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabHashLds<T, BS>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  auto go = [&](auto k, const auto* valA, int& per_cu) {
+  auto go = [&](auto k, const auto* valA) {
     set_lds(k, L);
-    if (!per_cu) {
-      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-      if (per_cu < 1) per_cu = 1;
-    }
+    const int per_cu = blocks_per_cu(k, BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                       A.n + 1, A.ir, valA, C.ir, C.val);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
+                       A.ir, valA, C.ir, C.val);
   };
-  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
-  if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp, per_cu_p);
-  else if (bp.valAf) go(k_num_slab_hash<SR, T, BS, false, float>, bp.valAf, per_cu_f);
-  else go(k_num_slab_hash<SR, T, BS, false, double>, A.val, per_cu_d);
+  // (A's exact f32 values come as (row, f32) records whenever they exist)
+  if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp);
+  else go(k_num_slab_hash<SR, T, BS, false, double>, A.val);
   df.take(queue);
 }
 
 template <int SR, int CAP, int BS>
-static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                               cbg_tile& C, hipStream_t s, DeferredFree& df) {
+static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
+                               const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabLds<CAP, BS>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  auto go = [&](auto k, const auto* valA, int& per_cu) {
+  auto go = [&](auto k, const auto* valA) {
     set_lds(k, L);
-    if (!per_cu) {
-      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, BS, L));
-      if (per_cu < 1) per_cu = 1;
-    }
+    const int per_cu = blocks_per_cu(k, BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.cmapP,
-                       A.n + 1, A.ir, valA, C.ir, C.val, bp.gbm.p, bp.cuts.p);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
+                       A.ir, valA, C.ir, C.val, bp.gbm.p, bp.cuts.p);
   };
-  static int per_cu_d[2] = {}, per_cu_f[2] = {}, per_cu_p[2] = {};
-  const int kk = bp.all_kept ? 1 : 0;
   if (bp.all_kept) {
-    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true>, bp.valAp, per_cu_p[kk]);
-    else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float, true>, bp.valAf, per_cu_f[kk]);
-    else go(k_num_slab<SR, CAP, BS, double, true>, A.val, per_cu_d[kk]);
+    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true>, bp.valAp);
+    else go(k_num_slab<SR, CAP, BS, double, true>, A.val);
   } else {
-    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false>, bp.valAp, per_cu_p[kk]);
-    else if (bp.valAf) go(k_num_slab<SR, CAP, BS, float, false>, bp.valAf, per_cu_f[kk]);
-    else go(k_num_slab<SR, CAP, BS, double, false>, A.val, per_cu_d[kk]);
+    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false>, bp.valAp);
+    else go(k_num_slab<SR, CAP, BS, double, false>, A.val);
   }
   df.take(queue);
 }
 
 template <int SR, int NCAP>
-static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A, const cbg_tile& B,
-                             cbg_tile& C, hipStream_t s, DeferredFree& df) {
+static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
+                             const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   constexpr int L = SlabRankLds<NCAP, RANK_BS>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
-  auto go = [&](auto k, const auto* valA, int& per_cu) {
+  auto go = [&](auto k, const auto* valA) {
     set_lds(k, L);
-    if (!per_cu) {
-      CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k, RANK_BS, L));
-      if (per_cu < 1) per_cu = 1;
-    }
+    const int per_cu = blocks_per_cu(k, RANK_BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, B.ir, B.val, bp.cmapP,
-                       A.n + 1, A.ir, valA, C.ir, C.val);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, B.ir, B.val, bp.pm(),
+                       A.ir, valA, C.ir, C.val);
   };
-  static int per_cu_d = 0, per_cu_f = 0, per_cu_p = 0;
-  if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV>, bp.valAp, per_cu_p);
-  else if (bp.valAf) go(k_num_slab_rank<SR, NCAP, RANK_BS, float>, bp.valAf, per_cu_f);
-  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double>, A.val, per_cu_d);
+  if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV>, bp.valAp);
+  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double>, A.val);
   df.take(queue);
 }
 
 // hash-mode single-panel slabs of more than this many nonzeros run as rank
-// slabs (CBG_RANK_MIN overrides; < 0: none)
-static int rank_slabs_min() {
-  static const char* e = getenv("CBG_RANK_MIN");
-  return e ? atoi(e) : 683;
-}
+// slabs (scale 24: 400 / 1000 measured 3789 / 3825 vs 3795 ms; scale 22 flat)
+constexpr int RANK_SLABS_MIN = 683;
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 
@@ -3205,6 +3239,7 @@ struct APrep {
   DBuf<int2> cmap, cmapP;  // cmapP: built by the first call that had big columns
   DBuf<unsigned char> clen8;  // A's column lengths clamped at 255
   int plog = -1;
+  bool kmajor = false;  // cmapP's layout
   DBuf<float> valf;  // A's values as f32 (af == 1)
   DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
@@ -3268,15 +3303,6 @@ static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned cha
   df.take(c_lo);
 }
 
-// CBG_APACK=0: the slab kernels read A's rows and f32 values from two arrays
-static bool apack_enabled() {
-  static const char* e = getenv("CBG_APACK");
-  return !(e && !strcmp(e, "0"));
-}
-static bool af32_enabled() {
-  static const char* e = getenv("CBG_AF32");
-  return !(e && !strcmp(e, "0"));
-}
 static APrep& aprep() {
   static thread_local APrep a;
   return a;
@@ -3313,6 +3339,7 @@ void local_spgemm(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_tile& 
   t.n_slabs += mine.n_slabs;
   t.ms_symbolic += mine.ms_symbolic;
   t.ms_numeric += mine.ms_numeric;
+  for (int i = 0; i < CBG_WORK_N; ++i) t.work[i] += mine.work[i];
   if (st) *st = mine;
 }
 
@@ -3352,17 +3379,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     CBG_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     CBG_HIP(hipEventCreateWithFlags(&ev_cjoin, hipEventDisableTiming));
   }
-  // CBG_SIDE=0/1/2/3: small-column bins of the symbolic (bit 0) / numeric (bit 1)
-  // on the side stream (default 3), else serialized on the main stream
-  static const int side_bits = getenv("CBG_SIDE") ? atoi(getenv("CBG_SIDE")) : 3;
-  const hipStream_t ssym = (side_bits & 1) ? side : s, snum = (side_bits & 2) ? side : s;
+  // the small-column bins of the symbolic and the numeric run on the side stream
+  // (serialized on the main one: -0.5 % at scale 22, -5 % at 18), the symbolic's
+  // on the main one where the big columns dominate (below)
+  const hipStream_t ssym = side, snum = side;
   auto fork = [&](hipStream_t main) {
     CBG_HIP(hipEventRecord(ev_fork, main));
     CBG_HIP(hipStreamWaitEvent(side, ev_fork, 0));
   };
-  // CBG_COPY_STREAM=0/1: the numeric's copies behind the side stream's bins /
-  // on a stream of their own (default: their own unless the big columns dominate)
-  static const int copy_stream_env = getenv("CBG_COPY_STREAM") ? atoi(getenv("CBG_COPY_STREAM")) : -1;
   auto join = [&](hipStream_t main) {
     CBG_HIP(hipEventRecord(ev_join, side));
     CBG_HIP(hipStreamWaitEvent(main, ev_join, 0));
@@ -3376,6 +3400,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   CBG_HIP(hipEventRecord(ev0, s));
   const int64_t nz = B.nzc;
+  int64_t work[CBG_WORK_N] = {};  // cbg_last_work_stats
+  reinterpret_cast<int64_t*>(host_stage(STAGE_SCALARS))[5] = 0;  // deferred group units (sync 2)
   // A column map (reused across the phases of one MemEfficientSpGEMM)
   APrep& ap = aprep();
   const uint64_t ser_ir = ap.active ? pool().serial_of(A.ir) : 0, ser_cp = ap.active ? pool().serial_of(A.cp) : 0;
@@ -3435,9 +3461,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // expected products per group; CBG_GROUPS=0 keeps every pair on its own)
   BigPlan bp;
   int64_t big_entries = 0, thin_entries = 0;  // B entries of the big / thin columns (read back with sync 1)
-  // small columns' symbolic and numeric in one pass (bins 1..SYM_FUSED_LAST), unless CBG_FUSE_SMALL=0
-  static const bool fuse_small = !(getenv("CBG_FUSE_SMALL") && !strcmp(getenv("CBG_FUSE_SMALL"), "0"));
-  const bool fused = fuse_small;
+  // small columns' symbolic and numeric in one pass (bins 1..SYM_FUSED_LAST)
+  constexpr bool fused = true;
   // single-entry columns as scaled copies of A's columns (CBG_COPY1=0: off)
   // (default 2: also those of more than `big` flops -- R-MAT columns whose one
   // entry hits a hub -- instead of (column, panel) pairs: s22 446.4 -> 440.9 ms;
@@ -3495,14 +3520,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   // inline records of A's columns for the small-column and thin passes when A's
   // columns are short (<= 2 entries on average) and each entry is gathered many
-  // times (flops >= 4 nnz(A)): GalerkinNew's S*(AT), S = T^T (CBG_AINL=0: off)
+  // times (flops >= 4 nnz(A)): GalerkinNew's S*(AT), S = T^T
   DBuf<int4> ainl;
   {
-    static const bool ainl_on = !(getenv("CBG_AINL") && !strcmp(getenv("CBG_AINL"), "0"));
     unsigned long long fsmall = 0;
     for (int b = 1; b < NSMALL; ++b) fsmall += sb.flops[b];
     fsmall += thin_R ? sb.flops[THIN_BIN] : 0;
-    if (ainl_on && fused && A.nnz <= 2 * A.nzc && (double)fsmall >= 4.0 * (double)A.nnz) {
+    if (fused && A.nnz <= 2 * A.nzc && (double)fsmall >= 4.0 * (double)A.nnz) {
       ainl.reset(2 * (A.n + 1));
       hipLaunchKernelGGL(k_inline_cols, dim3(nblk(A.n + 1, 256)), dim3(256), 0, s, A.n + 1, cmap.p, A.ir, A.val,
                          ainl.p);
@@ -3531,7 +3555,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       for (int b = 1; b < NSMALL; ++b) small_w += (double)sb.flops[b];
       big_dominant = main_w >= small_w;
     }
-    if (!getenv("CBG_SIDE") && big_dominant) sy = s;
+    if (big_dominant) sy = s;
     symst[0] = sy;
     balance_bins(sb.flops, 1, NSMALL - 1, main_w, 0.0, cost, s, sy, symst, !big_dominant);
   }
@@ -3554,13 +3578,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
           launch_esc<0>(at(b), sb.count[b], fmax_of(b), B, cmap.p, ainl.p, A, cnt.p, fused_ir.p, fused_val.p,
                         (int64_t)fused_off[b], fused_slot.p, symst[b]);
       }
-    } else {
-      for (int b = 1; b <= 5; ++b) launch_sym_wave<6>(at(b), sb.count[b], B, cmap.p, A, cnt.p, symst[b]);
-      for (int b = 6; b <= 7; ++b) launch_sym_wave<8>(at(b), sb.count[b], B, cmap.p, A, cnt.p, symst[b]);
-      launch_sym_wave<10>(at(8), sb.count[8], B, cmap.p, A, cnt.p, symst[8]);
     }
     static_assert(SYM_FUSED_LAST == 8 || SYM_FUSED_LAST == 9, "fused bins");
-    if (!fused || SYM_FUSED_LAST < 9) launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
+    if (SYM_FUSED_LAST < 9) launch_sym_wave<10>(at(9), sb.count[9], B, cmap.p, A, cnt.p, symst[9]);
     launch_sym_block<11, 256>(at(10), sb.count[10], B, cmap.p, ainl.p, A, cnt.p, symst[10]);
     launch_sym_block<12, 256>(at(11), sb.count[11], B, cmap.p, ainl.p, A, cnt.p, symst[11]);
     launch_sym_block<13, 512>(at(12), sb.count[12], B, cmap.p, ainl.p, A, cnt.p, symst[12]);
@@ -3577,9 +3597,9 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<PackedRV>& valp = ap.active ? ap.valp : valp_own;
   int af = ap.active ? ap.af : -1, af_inexact = 0;
   DBuf<int> af_flag;
-  if (nbig > 0 && af < 0 && af32_enabled() && !sym_only) {
+  if (nbig > 0 && af < 0 && !sym_only) {
     valf.reset(A.nnz);
-    if (apack_enabled()) valp.reset(A.nnz);
+    valp.reset(A.nnz);
     af_flag.reset(1);
     CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
     const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
@@ -3590,7 +3610,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
     constexpr int pm_entries = 64;  // map only the referenced A columns when big-column entries * 64 < A's columns
-    if (ap.active && ap.cmapP.p && ap.plog == bp.plog) {
+    bp.n1 = A.n + 1;
+    // column-major panel maps for the symbolic's XCD column order: a column's R
+    // entries in one or two lines (scale 22: 399.6 -> 395.5 ms alone, with the
+    // order 384 ms; the numeric slabs, panel-major, read them at the same speed)
+    bp.kmajor = bp.R > 1;
+    if (ap.active && ap.cmapP.p && ap.plog == bp.plog && ap.kmajor == bp.kmajor) {
       bp.cmapP = ap.cmapP.p;
     } else if (bp.R > 1 && pm_entries > 0 && big_entries * pm_entries < A.nzc) {
       // few big-column entries (GalerkinNew's A*T: ~10^3 of A's 4 M columns;
@@ -3600,7 +3625,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       // R x n map; this B's own map, never cached for other pieces / phases
       bp.cmapP_own.reset((size_t)bp.R * (A.n + 1));
       hipLaunchKernelGGL(k_colmap_panels_entries, dim3(nblk((int64_t)nbig * WAVE, 256)), dim3(256), 0, s,
-                         bp.perm_big, nbig, B.cp, B.ir, cmap.p, A.ir, bp.plog, bp.R, A.n + 1, bp.cmapP_own.p);
+                         bp.perm_big, nbig, B.cp, B.ir, cmap.p, A.ir, bp.plog, bp.R, bp.pm().sr, bp.pm().sk,
+                         bp.cmapP_own.p);
       bp.cmapP = bp.cmapP_own.p;
     } else {
       DBuf<int2>& cp = ap.active ? ap.cmapP : bp.cmapP_own;
@@ -3610,9 +3636,12 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       } else {
         CBG_HIP(hipMemsetAsync(cp.p, 0, sizeof(int2) * bp.R * (A.n + 1), s));
         hipLaunchKernelGGL(k_colmap_panels_col, dim3(nblk(A.nzc, 256)), dim3(256), 0, s, A.nzc, A.cp, A.jc, A.ir,
-                           bp.plog, bp.R, A.n + 1, cp.p);
+                           bp.plog, bp.R, bp.pm().sr, bp.pm().sk, cp.p);
       }
-      if (ap.active) ap.plog = bp.plog;
+      if (ap.active) {
+        ap.plog = bp.plog;
+        ap.kmajor = bp.kmajor;
+      }
       bp.cmapP = cp.p;
     }
     bp.desc.reset((size_t)nbr * NFINE_MAX);
@@ -3636,7 +3665,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     DBuf<unsigned long long> cuts_next;
     long long cuts_cap = 0;
     if (!sym_only) {
+      // at most min(1.5 GB, 2 % of the free HBM), and never more than the cuts of
+      // every pair cut into NFINE_MAX slabs (GalerkinNew's few big columns need
+      // little); CBG_CUTS_CAP (entries, read per call) is a test hook that leaves
+      // pairs past it to the numeric's searches
       cuts_cap = std::min<long long>(INT32_MAX, (long long)(std::min(1.5e9, 0.02 * device_bytes_available()) / 4));
+      cuts_cap = std::min<long long>(cuts_cap, (long long)big_entries * bp.R * (NFINE_MAX - 1));
+      if (const char* e = getenv("CBG_CUTS_CAP")) cuts_cap = std::min<long long>(cuts_cap, atoll(e));
       bp.cuts.reset(std::max<long long>(cuts_cap, 1));
       bp.pcoff.reset(nbr);
       cuts_next.reset(1);
@@ -3650,7 +3685,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     };
     set_lds(k_sym_panel<true>, lds_of(std::max(pwords, GROUP_T)));
     set_lds(k_sym_panel<false>, lds_of(std::max(pwords, GROUP_T)));
-    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.cmapP, A.n + 1, A.ir, A.m,
+    SymPanelArgs sa{bp.perm_big, bp.R, bp.plog, 0, 0, pwords, 0, B.cp, B.ir, bp.pm(), A.ir, A.m,
                     cnt.p, bp.cnt_br.p, bp.desc.p, bp.nslab.p, bp.gbm.p, (int)nslots, gbm_next.p,
                     bp.gbm_slot.p,
                     bp.cuts.p, cuts_next.p, cuts_cap,
@@ -3678,13 +3713,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       sa.hwords = sa.glog > 0 ? std::max(pwords, GROUP_T) : pwords;
       const int64_t RG = (bp.R + (1 << sa.glog) - 1) >> sa.glog;
       sa.ncls = nc;
-      static int per_cu = 0;  // resident blocks per CU at the largest LDS size
-      if (!per_cu) {
-        CBG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_sym_panel<true>, BIG_BS,
-                                                             lds_of(std::max(pwords, GROUP_T))));
-        if (per_cu < 1) per_cu = 1;
-      }
-      const int64_t grid = std::min<int64_t>(RG * nc, (int64_t)per_cu * device_cus() * CBG_SYM_WAVES_OF_UNITS);
+      work[sa.glog > 0 ? CBG_WORK_SYM_GROUP_UNITS : CBG_WORK_SYM_PANEL_UNITS] += RG * nc;
+      // resident blocks per CU at this launch's LDS size
+      const int per_cu = sa.glog > 0 ? blocks_per_cu(k_sym_panel<true>, BIG_BS, lds_of(sa.hwords))
+                                     : blocks_per_cu(k_sym_panel<false>, BIG_BS, lds_of(sa.hwords));
+      // (a multiple of 8: the XCD column order; 8 x ceil(nc / 8) x RG units)
+      const int64_t grid = std::min<int64_t>(RG * ((nc + 7) / 8) * 8,
+                                             ((int64_t)per_cu * device_cus() * CBG_SYM_WAVES_OF_UNITS) & ~7LL);
       if (sa.glog > 0)
         hipLaunchKernelGGL(k_sym_panel<true>, dim3((unsigned)grid), dim3(BIG_BS), lds_of(sa.hwords), s, sa);
       else
@@ -3695,6 +3730,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       set_lds(k_sym_deferred, lds_of(sa.hwords));
       hipLaunchKernelGGL(k_sym_deferred, dim3((unsigned)std::min<int64_t>(group_units, device_cus() * 4)),
                          dim3(BIG_BS), lds_of(sa.hwords), s, sa);
+      CBG_HIP(hipMemcpyAsync(reinterpret_cast<int64_t*>(host_stage(STAGE_SCALARS)) + 5, defer_n.p, sizeof(int),
+                             hipMemcpyDeviceToHost, s));
       df.take(defer);
       df.take(defer_n);
     }
@@ -3770,6 +3807,10 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   const int64_t nnzc = scal[0], nzcC = scal[2], flops_total = scal[3];
   nslabs = scal[1];
   const int64_t single_big_entries = scal[4];
+  work[CBG_WORK_SYM_DEFERRED_UNITS] = scal[5];
+  for (int b = 1; fused && b <= SYM_FUSED_LAST; ++b) work[CBG_WORK_ESC_COLUMNS] += sb.count[b];
+  work[CBG_WORK_THIN_COLUMNS] = thin_R ? sb.count[THIN_BIN] : 0;
+  work[CBG_WORK_SINGLE_BIG_ENTRIES] = copy1 > 1 ? single_big_entries : 0;
   if (sym_only) {
     df.synced = true;
     if (st) {
@@ -3780,6 +3821,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       st->nnz = nnzc;
       st->n_big = nbig;
       st->flops = flops_total;
+      std::memcpy(st->work, work, sizeof(work));
     }
     return;
   }
@@ -3816,7 +3858,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const int NK = SLAB_NCLS * slab_kr(bp.R);
     DBuf<int> counters(2 * NK + SLAB_NCLS);  // counts[NK] | cursor[NK] | class totals
     CBG_HIP(hipMemsetAsync(counters.p, 0, (2 * NK + SLAB_NCLS) * sizeof(int), s));
-    const int rank_span = rank_slabs_min() >= 0 ? 1 << bp.plog : 0, rank_min = rank_slabs_min();
+    const int rank_span = 1 << bp.plog, rank_min = RANK_SLABS_MIN;
     hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), NK * sizeof(int), s, nbig, bp.R, bp.nslab.p,
                        bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p);
     hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, bp.R, counters.p, counters.p + NK,
@@ -3831,8 +3873,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
       CBG_HIP(hipMemcpyAsync(ncls_h + SLAB_NCLS, bp.gbm_next, sizeof(int), hipMemcpyDeviceToHost, s));
     CBG_HIP(hipStreamSynchronize(s));  // host sync 3 of 4: the slab classes' sizes
     std::memcpy(ncls, ncls_h, sizeof(int) * SLAB_NCLS);
-    bp.all_kept = bp.gbm_next && (int64_t)ncls_h[SLAB_NCLS] <= bp.gbm_slots;
+    // (CBG_DBG bit 128 hands out slots without storing the bitmaps: the
+    // marking pass must run)
+    static const int dbg_kept = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
+    bp.all_kept = bp.gbm_next && (int64_t)ncls_h[SLAB_NCLS] <= bp.gbm_slots && !(dbg_kept & 128);
     df.take(counters);
+    work[bp.all_kept ? CBG_WORK_BITMAP_SMALL_KEPT : CBG_WORK_BITMAP_SMALL_MARK] = ncls[0];
+    work[bp.all_kept ? CBG_WORK_BITMAP_LARGE_KEPT : CBG_WORK_BITMAP_LARGE_MARK] = ncls[1];
+    for (int k = 0; k < SLAB_HASH_NCLS; ++k) work[CBG_WORK_HASH0 + k] = ncls[2 + k];
+    for (int k = 0; k < SLAB_RANK_NCLS; ++k) work[CBG_WORK_RANK0 + k] = ncls[SLAB_RANK0 + k];
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
     {
@@ -3857,12 +3906,14 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   // numeric
   Binned nbn;
   bin_scatter(nz, npend, nbn, s, df);
+  for (int b = 1; b <= 4; ++b) work[CBG_WORK_WAVE_BIN_COLUMNS] += nbn.count[b];
+  for (int b = 5; b <= 8; ++b) work[CBG_WORK_HASH_BIN_COLUMNS] += nbn.count[b];
   // small-column bins on the side stream, big-column slabs on the main one,
   // the copies (fused bins, single-entry columns) on the copy stream: they only
   // need colptr and stream at HBM rate beside the latency-bound kernels
   // (GalerkinNew at 22: 5.92 / 5.98 vs 6.45 / 6.38 ms); not where the big
   // columns' slabs dominate, which they slow (scale 22: 418.4 vs 413.0 ms)
-  const bool copy_stream = copy_stream_env >= 0 ? copy_stream_env > 0 : !big_dominant;
+  const bool copy_stream = !big_dominant;
   fork(s);
   const hipStream_t sc = copy_stream ? scopy : snum;
   if (copy_stream) CBG_HIP(hipStreamWaitEvent(scopy, ev_fork, 0));
@@ -3961,6 +4012,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     st->n_big = nbig;
     st->n_slabs = nslabs;
     st->flops = flops_total;  // total flops (k_flops), read back with sync 2
+    std::memcpy(st->work, work, sizeof(work));
   }
   Cg.release();  // completed: the caller owns C
 }

@@ -530,10 +530,8 @@ static void multiply_to_fn(const cbg_tile& A, const cbg_tile& B, int sr, hipStre
   if (r && !cb_rc) cb_rc = r;
 }
 
-static int comm_reserve_default() {
-  static const char* e = getenv("CBG_COMM_RESERVE_CUS");
-  return e ? std::max(0, atoi(e)) : 8;
-}
+// CUs the persistent slab kernels leave free while a broadcast is in flight
+static int comm_reserve_default() { return 8; }
 
 // one_phase: the cuts are pipeline pieces of ONE phase (fn gets phase 0 for
 // each of them, at its column offset), else piece p is phase p
@@ -727,7 +725,7 @@ static int summa_panel(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     local = step([&] {
       maybe_inject_fault(g);
       // piece p+1's broadcast runs on the comm stream during this multiply:
-      // the persistent kernels leave CBG_COMM_RESERVE_CUS (8) CUs to it
+      // the persistent kernels leave comm_reserve_default() (8) CUs to it
       CommReserve reserve(p + 1 < np && !g->host_mode ? comm_reserve_default() : 0);
       if (p == 0 && pc > 1) {
         std::vector<cbg_tile> parts(pc);
@@ -1064,7 +1062,7 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
   if (rc) return rc;
   mark("flops");
   // compression nnz/flops of a sample of this rank's product: one rank: every
-  // 64th column of B (CBG_PHASE_SAMPLE); a grid: every 8th row of the A block row
+  // 256th column of B; a grid: every 8th row of the A block row
   // times every 16th column of the B block column, the samples broadcast like
   // the SUMMA's tiles (1/8 and 1/16 of their bytes); ids, not positions, so the
   // tiles of a grid row / column sample the same rows / columns
@@ -1085,8 +1083,7 @@ static int plan_phases(cbg_grid* g, const cbg_tile& A, const cbg_tile& B, int64_
     return rc;
   double ratio = 1.0;
   if (need_sample) {
-    static const char* es = getenv("CBG_PHASE_SAMPLE");
-    const int cstride = es ? std::max(1, atoi(es)) : (g->nranks == 1 ? 256 : 16);
+    const int cstride = g->nranks == 1 ? 256 : 16;
     const int rstride = g->nranks == 1 ? 1 : 8;
     TileGuard As, Bs;
     rc = agree(g, step([&] {

@@ -99,11 +99,35 @@ bool DevicePool::release_largest_cached() {
   return true;
 }
 
+DevicePool::DevicePool() {
+  const char* e = getenv("CBG_POOL_QUARANTINE");
+  quarantine_ = e && atoi(e) > 0;
+}
+
+void DevicePool::quarantine_release() {
+  if (!quarantine_) return;
+  (void)hipDeviceSynchronize();  // no kernel uses a quarantined block any more, the poison has landed
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto& q : quar_) {
+    free_.emplace(q.second, q.first);
+    cached_ += q.second;
+  }
+  quar_.clear();
+}
+
 void DevicePool::free(void* p) {
   if (!p) return;
   std::lock_guard<std::mutex> lk(mu_);
   serial_.erase(p);
   auto it = live_.find(p);
+  if (it != live_.end() && quarantine_) {
+    if (!poison_) (void)hipStreamCreateWithFlags(&poison_, hipStreamNonBlocking);
+    (void)hipMemsetAsync(p, 0xff, it->second, poison_);
+    quar_.emplace_back(p, it->second);
+    in_use_ -= it->second;
+    live_.erase(it);
+    return;
+  }
   if (it == live_.end()) {
     auto g = grow_.find(p);
     if (g != grow_.end()) {  // keep it mapped for the next growable request

@@ -161,6 +161,32 @@ int cbg_merge(const cbg_tile* parts, int nparts, int semiring, cbg_tile* C, void
  * per-phase device ms, big columns, slabs.  Merges are not counted here. */
 int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms_numeric, int64_t* n_big,
                    int64_t* n_slabs);
+/* ... and the work of each kernel family (summed over the call's multiplies), so a
+ * test can prove which code paths ran: numeric slabs per launch class (bitmap
+ * slabs with kept symbolic bitmaps / with the marking pass, hash slabs by table
+ * size 512 ... 8192, rank slabs of <= 1024 / 2048 / 4096 nonzeros), symbolic
+ * (column, panel) units and panel-group units, group units run panel by panel,
+ * columns of the one-pass small-column kernels, thin columns, entries of the
+ * single-entry big columns, columns of the numeric hash / wave bins.
+ * counts[i] for i < min(n, CBG_WORK_N); returns CBG_WORK_N. */
+enum {
+  CBG_WORK_BITMAP_SMALL_KEPT = 0,
+  CBG_WORK_BITMAP_SMALL_MARK = 1,
+  CBG_WORK_BITMAP_LARGE_KEPT = 2,
+  CBG_WORK_BITMAP_LARGE_MARK = 3,
+  CBG_WORK_HASH0 = 4, /* + k: tables of 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192 slots */
+  CBG_WORK_RANK0 = 13, /* + k: rank slabs of <= 1024, 2048, 4096 nonzeros */
+  CBG_WORK_SYM_PANEL_UNITS = 16,
+  CBG_WORK_SYM_GROUP_UNITS = 17,
+  CBG_WORK_SYM_DEFERRED_UNITS = 18,
+  CBG_WORK_ESC_COLUMNS = 19,
+  CBG_WORK_THIN_COLUMNS = 20,
+  CBG_WORK_SINGLE_BIG_ENTRIES = 21,
+  CBG_WORK_HASH_BIN_COLUMNS = 22,
+  CBG_WORK_WAVE_BIN_COLUMNS = 23,
+  CBG_WORK_N = 24
+};
+int cbg_last_work_stats(int64_t* counts, int n);
 /* last call's multiway merges (MergeAll / MultiwayMerge): partial entries in,
  * merged entries out, device ms */
 int cbg_merge_stats(int64_t* entries_in, int64_t* entries_out, double* ms);

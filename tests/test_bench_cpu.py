@@ -59,3 +59,23 @@ def test_default_grids_and_flags():
     assert b.GRIDS[1] == (1, 1) and b.GRIDS[2][0] * b.GRIDS[2][1] == 2 and b.GRIDS[8][0] * b.GRIDS[8][1] == 8
     src = open(os.path.join(REPO, "bench.py")).read()
     assert "--no-f64-leg" in src and "frac_f64_values" in src
+
+
+def test_newest_profile_lookup(tmp_path):
+    """the CPU-baseline and traffic records come from the highest round present
+    (a hard-coded round list skipped r04)"""
+    import json
+    b = load_bench()
+    for rnd, v in (("r02", 65.6e6), ("r04", 68.9e6), ("r10", 70.0e6), ("r03", 1.0)):
+        (tmp_path / ("%s_cpu_reference_s22.json" % rnd)).write_text(json.dumps({"value": v}))
+    (tmp_path / "r11_cpu_reference_s22.json").write_text("not json")
+    d, path = b.newest_profile("cpu_reference_s22.json", lambda d: "value" in d, root=str(tmp_path))
+    assert d["value"] == 70.0e6 and path.endswith("r10_cpu_reference_s22.json")
+    # a predicate skips records of other configurations
+    d, _ = b.newest_profile("cpu_reference_s22.json", lambda d: d["value"] < 69e6, root=str(tmp_path))
+    assert d["value"] == 68.9e6
+    # the committed records: the newest round's s22 reference run
+    s22 = b.cpu_baseline_s22()
+    rounds = sorted(int(n[1:3]) for n in os.listdir(os.path.join(REPO, "profiles"))
+                    if n.endswith("_cpu_reference_s22.json"))
+    assert s22["source"] == "profiles/r%02d_cpu_reference_s22.json" % rounds[-1]

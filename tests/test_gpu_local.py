@@ -666,9 +666,14 @@ def test_phase_split_on_oom(cbg):
 
 
 @pytest.mark.parametrize("env", [{"CBG_BITMAP_BUDGET_GB": "0"}, {"CBG_BIG_FLOPS": "64"},
-                                 {"CBG_BIG_FLOPS": "64", "CBG_BITMAP_BUDGET_GB": "0"}])
+                                 {"CBG_BIG_FLOPS": "64", "CBG_BITMAP_BUDGET_GB": "0"},
+                                 {"CBG_BITMAP_BUDGET_GB": "0.0002"}, {"CBG_CUTS_CAP": "3000"},
+                                 {"CBG_CUTS_CAP": "0"}])
 def test_big_column_path_variants(env):
-    """Same products through the other big-column code paths (subprocess: knobs are read once)."""
+    """Same products through the other big-column code paths (subprocess: knobs are
+    read once): no kept bitmaps; a budget for a few of them (the general k_num_slab
+    with kept and marked slabs mixed); multi-slab pairs' cuts for the first pairs only
+    (the others search theirs: both kinds in one launch) or for none."""
     import json
     import os
     import subprocess
@@ -1144,6 +1149,15 @@ def test_random_values_scale20_vs_oracle(cbg, sr):
     C = cbg.LocalHybridSpGEMM(A, B, sr)
     st = cbg.last_stats()
     assert st["n_big"] > 0 and st["n_slabs"] > 0, st
+    w = cbg.last_work_stats()
+    # the f64-value instantiations of every family this shape reaches ran:
+    # (column, panel) units and panel groups in the symbolic, bitmap slabs with
+    # kept bitmaps (both classes), rank and hash slabs, the small-column passes
+    for k in ("sym_panel_units", "sym_group_units", "bitmap_small_kept", "bitmap_large_kept", "esc_columns",
+              "hash_bin_columns"):
+        assert w[k] > 0, (k, w)
+    assert sum(w["rank_N%d" % n] for n in (1024, 2048, 4096)) > 0, w
+    assert sum(w["hash_T%d" % t] for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)) > 0, w
     Ch = C.to_host()
     C.free()
     ref = oracle_local(Ah, Bh, sr)
@@ -1192,6 +1206,7 @@ def test_random_values_scale22_pieces_vs_oracle(cbg):
     n = 1 << 22
     A = cbg.rmat_tile(22, 16).set_random_values()
     Ah = A.to_host()
+    work = None
     for p in S22_VALUE_PIECES:
         c0, c1 = p * (n // 512), (p + 1) * (n // 512)
         left, right = A.split_cols(c1)
@@ -1204,6 +1219,8 @@ def test_random_values_scale22_pieces_vs_oracle(cbg):
             C = cbg.LocalHybridSpGEMM(A, B, sr)
             st = cbg.last_stats()
             assert st["n_big"] > 0 and st["n_slabs"] > 0, (p, st)
+            w = cbg.last_work_stats()
+            work = w if work is None else {k: work[k] + w[k] for k in w}
             Ch = C.to_host()
             C.free()
             ref = oracle_local(Ah, Bh, sr)
@@ -1213,6 +1230,87 @@ def test_random_values_scale22_pieces_vs_oracle(cbg):
                 assert_tiles_equal(Ch, ref)
         B.free()
     A.free()
+    # every kernel family the docstring names ran with f64 values: symbolic units
+    # and panel groups, both bitmap slab classes (kept bitmaps), all three rank
+    # classes, several hash-slab table sizes
+    for k in ("sym_panel_units", "sym_group_units", "bitmap_small_kept", "bitmap_large_kept", "rank_N1024",
+              "rank_N2048", "rank_N4096"):
+        assert work[k] > 0, (k, work)
+    assert sum(1 for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192) if work["hash_T%d" % t]) >= 3, work
+
+
+def _subprocess_local(env, code, timeout=600):
+    """run `code` (prints one JSON line last) in a fresh process with `env` (the
+    library reads its knobs once per process)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **env), cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_random_values_scale22_piece_marking_pass(cbg, tmp_path):
+    """The general k_num_slab (no kept bitmaps: the numeric marks its rows itself)
+    with f64 values at the headline's shape: CBG_BITMAP_BUDGET_GB=0, scale-22 R-MAT
+    with U[-1,1) values, B-column piece 230 of 512; entry by entry against the
+    oracle within 1e-12 (|A||B|)_ij."""
+    n = 1 << 22
+    p = 230
+    out = str(tmp_path / "c.npz")
+    code = r"""
+import sys, json, numpy as np
+sys.path.insert(0, "tests")
+from conftest import load_cbg
+cbg = load_cbg()
+n = 1 << 22
+A = cbg.rmat_tile(22, 16).set_random_values()
+left, right = A.split_cols(%d); right.free()
+low, B = left.split_cols(%d); low.free(); left.free()
+C = cbg.LocalHybridSpGEMM(A, B)
+w = cbg.last_work_stats()
+Ch = C.to_host()
+np.savez(%r, **{k: Ch[k] for k in ("cp", "jc", "ir", "val")})
+print(json.dumps(w))
+""" % ((p + 1) * (n // 512), p * (n // 512), out)
+    w = _subprocess_local({"CBG_BITMAP_BUDGET_GB": "0"}, code)
+    assert w["bitmap_small_mark"] > 0 and w["bitmap_large_mark"] > 0, w
+    assert w["bitmap_small_kept"] == 0 and w["bitmap_large_kept"] == 0, w
+    z = np.load(out)
+    Ch = dict(m=n, n=n // 512, cp=z["cp"], jc=z["jc"], ir=z["ir"], val=z["val"])
+    A = cbg.rmat_tile(22, 16).set_random_values()
+    Ah = A.to_host()
+    A.free()
+    Bh = _cols_host(Ah, lambda j: (j >= p * (n // 512)) & (j < (p + 1) * (n // 512)))
+    Bh["n"] = n // 512
+    Bh["jc"] = Bh["jc"] - p * (n // 512)
+    ref = oracle_local(Ah, Bh)
+    assert_tiles_equal(Ch, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+
+
+def test_pool_quarantine_scale20(cbg):
+    """The pool's debug quarantine (CBG_POOL_QUARANTINE=1: a freed block is poisoned
+    at once on another stream and not reused before the multiply's end), so a
+    buffer released while a kernel can still read it would corrupt the product: the
+    scale-20 A*A digest still equals the oracle's, rows sorted."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_large.json")) as f:
+        g = json.load(f)["s20_ef16"]
+    code = r"""
+import sys, json
+sys.path.insert(0, "tests")
+from conftest import load_cbg
+cbg = load_cbg()
+A = cbg.rmat_tile(20, 16); B = cbg.rmat_tile(20, 16)
+C = cbg.LocalHybridSpGEMM(A, B)
+d = C.digest()
+print(json.dumps({k: d[k] for k in ("nnz", "nzc", "hs", "hv", "unsorted")}))
+"""
+    d = _subprocess_local({"CBG_POOL_QUARANTINE": "1"}, code)
+    assert (d["nnz"], d["nzc"], d["hs"], d["hv"], d["unsorted"]) == (g["nnz"], g["nzc"], g["hs"], g["hv"], 0), (d, g)
 
 
 def test_local_scale24_column_pieces_vs_oracle(cbg):
