@@ -76,7 +76,7 @@ EXPORTS = [
     "cbg_grid_transpose", "cbg_grid_block_extract", "cbg_grid_agree", "cbg_merge_stats", "cbg_tile_alloc",
     "cbg_tile_concat_cols", "cbg_device_memory", "cbg_last_summa_info", "cbg_summa_spgemm_memeff",
     "cbg_last_summa_comm",
-    "cbg_last_phase_plan", "cbg_last_work_stats",
+    "cbg_last_phase_plan", "cbg_last_work_stats", "cbg_store_probe",
 ]
 Column, Row = 0, 1  # DimApply dimensions (SpDefs.h Dim)
 OP_MULTIPLIES, OP_PLUS, OP_MIN, OP_MAX = 0, 1, 2, 3
@@ -122,6 +122,7 @@ def lib():
         "cbg_last_stats": ([ctypes.POINTER(i64), ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ctypes.POINTER(i64)], i32),
         "cbg_last_work_stats": ([ctypes.POINTER(i64), i32], i32),
+        "cbg_store_probe": ([i64, i32], i32),
         "cbg_get_unique_id": ([vp], i32),
         "cbg_grid_create": ([i32, i32, i32, i32, vp, ctypes.POINTER(vp)], i32),
         "cbg_grid_create_host": ([i32, i32, i32, i32, ctypes.POINTER(CHostComm), ctypes.POINTER(vp)], i32),
@@ -469,6 +470,12 @@ def hbm_copy_bandwidth(nbytes=4 << 30, reps=10):
     g = ctypes.c_double()
     _check(lib().cbg_hbm_copy_bandwidth(nbytes, reps, ctypes.byref(g)))
     return g.value
+
+
+def store_probe(nbytes, width):
+    """writes exactly nbytes of a scratch buffer with width-byte (4 or 8) stores per
+    lane, lane-consecutive (the WRITE_SIZE calibration of tools/traffic.py)"""
+    _check(lib().cbg_store_probe(nbytes, width))
 
 
 def device_count():

@@ -105,6 +105,15 @@ int cbg_hbm_copy_bandwidth(int64_t bytes, int reps, double* gbps) {
   });
 }
 
+int cbg_store_probe(int64_t bytes, int width) {
+  if (bytes <= 0 || bytes % 256 || (width != 4 && width != 8))
+    return fail(CBG_ERR_INVALIDPARAMS, "cbg_store_probe: bytes a positive multiple of 256, width 4 or 8");
+  return guard([&] {
+    cbg::store_probe(bytes, width);
+    return CBG_OK;
+  });
+}
+
 int cbg_synchronize(void) {
   return guard([&] {
     CBG_HIP(hipDeviceSynchronize());

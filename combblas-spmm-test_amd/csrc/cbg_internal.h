@@ -314,5 +314,6 @@ void tile_random_values(cbg_tile& t, uint64_t seed, int64_t roff, int64_t coff, 
 
 // measured HBM bandwidth: 16-B-per-lane device copy (cbg_ops.hip)
 double hbm_copy_gbps(int64_t bytes, int reps);
+void store_probe(int64_t bytes, int width);
 
 }  // namespace cbg

@@ -7,6 +7,7 @@
 //                      nonzeros per fine row in uniform coarse columns, values in (0,1])
 // Sorts: cbg_sort.hip (radix sort over the key bits that vary, 64-bit counts).
 #include <algorithm>
+#include <type_traits>
 
 #include "cbg_device.h"
 #include "cbg_internal.h"
@@ -300,6 +301,23 @@ __global__ __launch_bounds__(256) void k_copy16_flat(const uint4* __restrict__ s
 // streaming the buffer with 1 / 4 / 8 loads per lane), swept on the first call
 // and the winner reused (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy).
 // Bytes moved = 2 x the buffer.
+// WRITE_SIZE calibration: n stores of W bytes, lane-consecutive, grid-stride
+template <int W>
+__global__ __launch_bounds__(256) void k_store_probe(char* __restrict__ dst, int64_t n) {
+  using T = typename std::conditional<W == 4, int, long long>::type;
+  T* d = reinterpret_cast<T*>(dst);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    d[i] = (T)i;
+}
+void store_probe(int64_t bytes, int width) {
+  DBuf<char> buf(bytes);
+  const int64_t n = bytes / width;
+  const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 256 * 64);
+  if (width == 4) hipLaunchKernelGGL(k_store_probe<4>, dim3(g), dim3(256), 0, nullptr, buf.p, n);
+  else hipLaunchKernelGGL(k_store_probe<8>, dim3(g), dim3(256), 0, nullptr, buf.p, n);
+  CBG_HIP(hipDeviceSynchronize());
+}
+
 double hbm_copy_gbps(int64_t bytes, int reps) {
   const int64_t n = std::max<int64_t>(bytes / 16, 1);
   DBuf<uint4> ba(n), bb(n);  // from the pool (it drops its cache and retries when the device is full)

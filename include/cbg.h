@@ -82,6 +82,11 @@ int cbg_synchronize(void);
 /* measured side of the HBM roofline (no reference counterpart): a 16-byte-per-lane
  * device copy of `bytes` run `reps` times; *gbps = 2 * bytes * reps / time (GB/s) */
 int cbg_hbm_copy_bandwidth(int64_t bytes, int reps, double* gbps);
+/* known-bytes store probe for the PMC traffic calibration (tools/traffic.py, no
+ * reference counterpart): writes exactly `bytes` (a multiple of 256) of a scratch
+ * buffer with `width`-byte stores (4 or 8) per lane -- the SpGEMM kernels' C row
+ * ids and values -- consecutive lanes at consecutive addresses (k_store_probe<W>) */
+int cbg_store_probe(int64_t bytes, int width);
 
 /* ---------------- tiles ---------------- */
 /* host -> device copy (arrays of *dst are allocated by libcbg) */

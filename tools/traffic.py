@@ -14,8 +14,16 @@ digests are the calibration: k_digest reads A's DCSC arrays once, wave per
 column, 4-8 B per lane -- the same access widths as the SpGEMM kernels -- so
 known_bytes / FETCH bytes of digest(A) corrects the gfx950 FETCH_SIZE
 under-count (MI355X_MICROARCH.md, HBM section: FETCH_SIZE reports 1/2 of a wide
-coalesced read; other widths uncalibrated).  WRITE_SIZE is reported as read
-(no store-width calibration is available for 4-8 B/lane stores).
+coalesced read; other widths uncalibrated).  WRITE_SIZE: after the last digest
+`run` stores known byte counts with 4- and 8-byte stores per lane (k_store_probe,
+the widths of C's row ids and values; the kept bitmaps are 16-byte stores, which
+the guide finds exact) and a wave-per-column 8-byte store of A's values
+(k_random_values: C's per-column runs), so the parse reports WRITE_SIZE's factor
+for each width; the write total is corrected with the 4-/8-byte factors applied to
+C's known row-id and value bytes (the rest taken as read).
+The algorithmic bytes split as SURVEY 8(d): symbolic 4 F + 12 N_B (A's rows per
+product, B's entries and map hops), numeric 12 F + 12 N_C + 20 N_B + 8 n; the
+per-phase ratios compare the symbolic and numeric kernels' traffic with them.
 """
 import argparse
 import csv
@@ -77,7 +85,14 @@ def run(a):
         st = cbg.last_stats()
         C.digest()
         cnnz, cnzc = C.nnz, C.nzc
-    meta = {"scale": a.scale, "ef": a.ef, "phases": a.phases,
+    # WRITE_SIZE calibration (after the 3rd digest): known bytes at 4 and 8 B per lane,
+    # and 8-byte values written wave per column (A's values, 8 nnz(A) bytes)
+    probe = 1 << 30
+    cbg.store_probe(probe, 4)
+    cbg.store_probe(probe, 8)
+    A.set_random_values()
+    cbg.synchronize()
+    meta = {"store_probe_bytes": probe, "scale": a.scale, "ef": a.ef, "phases": a.phases,
             "A": {"nnz": A.nnz, "nzc": A.nzc}, "B": {"nnz": B.nnz, "nzc": B.nzc, "n": B.n},
             "C": {"nnz": cnnz, "nzc": cnzc}, "flops": st["flops"]}
     print(json.dumps(meta), flush=True)
@@ -115,9 +130,19 @@ def parse(a):
             meta = json.loads(line)
     fr = read_pmc(a.fetch, "FETCH_SIZE")
     wr = read_pmc(a.write, "WRITE_SIZE")
+    kb = 1024.0  # rocprofv3 FETCH_SIZE / WRITE_SIZE unit: KiB
+    wcal = {}
+    if "store_probe_bytes" in meta:
+        pb = meta["store_probe_bytes"]
+        for w in (4, 8):
+            v = [x for _, n, x in wr if "k_store_probe<%d>" % w in n]
+            if v:
+                wcal["lane_%dB" % w] = pb / (v[-1] * kb)
+        v = [x for _, n, x in wr if "k_random_values" in n]
+        if v:
+            wcal["column_runs_8B"] = 8 * meta["A"]["nnz"] / (v[-1] * kb)
     d0, d1, _, mult_f = split(fr)
     _, _, _, mult_w = split(wr)
-    kb = 1024.0  # rocprofv3 FETCH_SIZE / WRITE_SIZE unit: KiB
     known_a = tile_bytes(meta["A"])
     calib = known_a / (0.5 * (d0[2] + d1[2]) * kb)
     fetch_raw = sum(v for _, _, v in mult_f) * kb
@@ -131,17 +156,33 @@ def parse(a):
         per_kernel.setdefault(k, [0.0, 0.0])[1] += v * kb
     F, nnzc, nnzb, n = meta["flops"], meta["C"]["nnz"], meta["B"]["nnz"], meta["B"]["n"]
     alg = 16 * F + 12 * nnzc + 32 * nnzb + 8 * n
+    # the writes with a calibrated width: C's row ids (4 B) and values (8 B); the
+    # rest (kept bitmaps in 16-byte stores, column pointers, temporaries) as read
+    write = write_raw
+    if "lane_4B" in wcal and "lane_8B" in wcal:
+        c4, c8 = 4.0 * nnzc, 8.0 * nnzc
+        write = write_raw - c4 / wcal["lane_4B"] - c8 / wcal["lane_8B"] + c4 + c8
+    # per phase: symbolic (k_sym*) and the rest (numeric, copies, scans) against
+    # SURVEY 8(d)'s split of the algorithmic bytes
+    alg_sym = 4 * F + 12 * nnzb
+    sym_t = sum(f + w for k, (f, w) in per_kernel.items() if "k_sym" in k)
+    num_t = sum(f + w for k, (f, w) in per_kernel.items() if "k_sym" not in k)
+    phases = {"symbolic": {"counter_bytes": sym_t, "algorithmic_bytes": alg_sym, "ratio": sym_t / alg_sym},
+              "numeric": {"counter_bytes": num_t, "algorithmic_bytes": alg - alg_sym, "ratio": num_t / (alg - alg_sym)}}
     out = {"scale": meta["scale"], "ef": meta["ef"], "phases": meta.get("phases", 1), "dispatches": len(mult_f),
            "fetch_calibration": calib, "fetch_bytes_raw": fetch_raw, "fetch_bytes": fetch_raw * calib,
-           "write_bytes": write_raw, "traffic_bytes": fetch_raw * calib + write_raw,
-           "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_raw * calib + write_raw) / alg,
+           "write_calibration": wcal, "write_bytes_raw": write_raw,
+           "write_bytes": write, "traffic_bytes": fetch_raw * calib + write,
+           "algorithmic_bytes": alg, "traffic_over_algorithmic": (fetch_raw * calib + write) / alg,
+           "per_phase": phases,
            "per_kernel_fetch_write": {k: [round(x), round(y)] for k, (x, y) in
                                       sorted(per_kernel.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))},
            "meta": meta}
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps({k: out[k] for k in ("fetch_calibration", "fetch_bytes", "write_bytes", "traffic_bytes",
-                                          "algorithmic_bytes", "traffic_over_algorithmic")}))
+    print(json.dumps({k: out[k] for k in ("fetch_calibration", "write_calibration", "fetch_bytes", "write_bytes",
+                                          "traffic_bytes", "algorithmic_bytes", "traffic_over_algorithmic",
+                                          "per_phase")}))
 
 
 def main():
