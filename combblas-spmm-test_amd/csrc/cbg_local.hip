@@ -1183,7 +1183,9 @@ __global__ __launch_bounds__(BIG_BS) CBG_SYM_WPE_ATTR void k_sym_panel(SymPanelA
   // L2 hits 27.6 -> 44.5 % (single panels) and 13.9 -> 40.1 % (groups), the
   // kernel 87 -> 72.7 ms per scale-22 step (profiles/r06_l2_s22_*.txt).  The
   // panel-major order before kept every block on one panel, reusing the hub
-  // columns' runs in the Infinity Cache instead.
+  // columns' runs in the Infinity Cache instead; bands of 8 / 4 / 2 panels
+  // (column order inside a band) were 0.3 / 0.6 / 1.7 % slower than the whole
+  // column (profiles/r06_ab_sym_bands.json).
   // false: no unit left for this block
   auto start = [&](int unit) {
     stage = -1;
@@ -2037,12 +2039,19 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (staged(r) && tid < r.nb) p_ce = pm.at(r.r, p_ir);
   };
   SlabRec rec = list[i];
+  // (thread 0) the dequeue in flight: the slab after the next one -- issued a
+  // slab ahead, so its returning atomic is not waited for at a slab's start
+  int qnext = 0;
+  if (tid == 0) qnext = (int)gridDim.x + atomicAdd(queue, 1);
   fetch_words(rec);
   fetch_stage1(rec);
   fetch_stage2(rec);
   while (true) {
     // ---- next work item (its record arrives while this slab fills LDS)
-    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    if (tid == 0) {
+      tmp[NW + 2] = qnext;  // the next slab (dequeued during this block's previous slab)
+      qnext = (int)gridDim.x + atomicAdd(queue, 1);
+    }
     const int nout = rec.nout;
     const int lo = rec.lo, hi = rec.hi;
     const int words = rec_words(rec);
@@ -2359,14 +2368,20 @@ struct SlabHashLds {
 #endif
 // CMLEN: cmapP entries are (start, len) -- the whole-column map of the
 // column bins -- instead of the panel maps' (first, end)
-template <int SR, int TT, int BS, bool CMLEN, typename VA = double>
+// INL (with CMLEN): A's columns as inline records (k_inline_cols): an entry of
+// B whose A column holds <= 2 entries adds its products at once from the
+// record (no map hop, no gathers of A, no staging); the longer ones are staged
+// as usual, and a chunk without any skips the scan
+template <int SR, int TT, int BS, bool CMLEN, typename VA = double, bool INL = false>
 __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                       int plog, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB, PMap pm,
                                                       const int32_t* __restrict__ irA,
                                                       const VA* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir,
-                                                      double* __restrict__ out_val) {
+                                                      double* __restrict__ out_val,
+                                                      const int4* __restrict__ ainl = nullptr) {
+  static_assert(!INL || CMLEN, "inline A records: whole-column slabs only");
   // persistent blocks over a queue of hash slabs; the next slab's record and
   // B staging (irB/valB, then the A column map hop) are prefetched into
   // registers while the current slab multiplies and emits (see k_num_slab)
@@ -2393,7 +2408,7 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
   int p_ir0 = 0, p_ir1 = 0;
   double p_bv0 = 0.0, p_bv1 = 0.0;
   int2 p_ce0 = make_int2(0, 0), p_ce1 = make_int2(0, 0);
-  auto staged = [&](const SlabRec& r) { return r.nb <= PF * BS; };
+  auto staged = [&](const SlabRec& r) { return !INL && r.nb <= PF * BS; };
   auto fetch1 = [&](const SlabRec& r) {
     if (!staged(r)) return;
     if (tid < r.nb) {
@@ -2420,10 +2435,17 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
     if (PF > 1 && BS + tid < r.nb) p_ce1 = seg_of(r, p_ir1);
   };
   SlabRec rec = list[i];
+  // (thread 0) the dequeue in flight: the slab after the next one -- issued a
+  // slab ahead, so its returning atomic is not waited for at a slab's start
+  int qnext = 0;
+  if (tid == 0) qnext = (int)gridDim.x + atomicAdd(queue, 1);
   fetch1(rec);
   fetch2(rec);
   while (true) {
-    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    if (tid == 0) {
+      tmp[NW + 2] = qnext;  // the next slab (dequeued during this block's previous slab)
+      qnext = (int)gridDim.x + atomicAdd(queue, 1);
+    }
     const bool pre = staged(rec);
     unsigned long long tmark = wall_clock64();
     if (CBG_VEC_INIT) {  // 16-byte LDS stores (T is a multiple of 256; vals and keys are 16-byte aligned)
@@ -2450,7 +2472,27 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
       const int64_t p = rec.p0 + (int64_t)c * BS + tid;
       int s = 0, len = 0;
       double bval = 0.0;
-      if (p < p1) {
+      if (INL) {
+        if (p < p1) {
+          const int k = irB[p];
+          bval = valB[p];
+          const int4 r = ainl[2 * (int64_t)k];
+          if (r.x <= 2) {
+            if (r.x >= 1) {
+              const int4 v = ainl[2 * (int64_t)k + 1];
+              hash_acc_t<SR, T>(keys, vals, r.y, Sem<SR>::mul(__hiloint2double(v.y, v.x), bval));
+              if (r.x == 2) hash_acc_t<SR, T>(keys, vals, r.z, Sem<SR>::mul(__hiloint2double(v.w, v.z), bval));
+            }
+          } else {
+            s = r.y;
+            len = r.x;
+          }
+        }
+        if (!__syncthreads_or(len > 0)) {
+          if (c == nch - 1 && has_next) fetch1(nrec);
+          continue;
+        }
+      } else if (p < p1) {
         int2 ce;
         if (pre) {
           ce = c == 0 ? p_ce0 : p_ce1;
@@ -2542,6 +2584,7 @@ struct SlabRankLds {
   static_assert(SEG_BYTES % 16 == 0 && BM_OFF % 16 == 0 && GPRE_OFF % 16 == 0, "rank slab LDS alignment");
 };
 constexpr int RANK_BS = 512;
+static_assert(4096 <= SLAB_WORDS, "a rank slab's rows (<= 4096) are written into its bitmap's words");
 // a rank slab stages one B entry per thread: the symbolic's sparse pairs (the
 // rank slabs' source, sym_pair) have <= BIG_BS B entries
 static_assert(BIG_BS <= RANK_BS, "rank slabs stage <= RANK_BS B entries");
@@ -2589,10 +2632,17 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
     if (tid < r.nb) p_ce = pm.at(r.r, p_ir);
   };
   SlabRec rec = list[i];
+  // (thread 0) the dequeue in flight: the slab after the next one -- issued a
+  // slab ahead, so its returning atomic is not waited for at a slab's start
+  int qnext = 0;
+  if (tid == 0) qnext = (int)gridDim.x + atomicAdd(queue, 1);
   fetch1(rec);
   fetch2(rec);
   while (true) {
-    if (tid == 0) tmp[NW + 2] = (int)gridDim.x + atomicAdd(queue, 1);
+    if (tid == 0) {
+      tmp[NW + 2] = qnext;  // the next slab (dequeued during this block's previous slab)
+      qnext = (int)gridDim.x + atomicAdd(queue, 1);
+    }
     unsigned long long tmark = wall_clock64();
     const int lo = rec.lo, nout = rec.nout;
     const int ng = (((rec.hi - lo + 31) >> 5) + 3) >> 2;
@@ -2668,7 +2718,10 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
     }
     __syncthreads();
     phase_mark(tmark, 18);
-    // 3. accumulate at the ranks (all lookups first, then the atomics)
+    // 3. accumulate at the ranks (all lookups first, then the atomics); each
+    // product also writes its row at its rank into the bitmap's words, which
+    // no lookup reads any more after the barrier (duplicates write the same
+    // row), so C's rows come out in order with a coalesced copy
     {
       int rk[RK];
 #pragma unroll
@@ -2686,32 +2739,25 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
           rk[k] = x;
         }
       }
+      __syncthreads();
+      int* rows = reinterpret_cast<int*>(bm);  // [nout] (nout <= NCAP <= SLAB_WORDS)
 #pragma unroll
       for (int k = 0; k < RK; ++k)
-        if (rk[k] >= 0) Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
+        if (rk[k] >= 0) {
+          Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
+          rows[rk[k]] = lo + xr[k];
+        }
     }
     if (has_next) fetch2(nrec);
     __syncthreads();
     phase_mark(tmark, 19);
-    // 4. rows from the bitmap (sorted), values from vals
+    // 4. rows and values in rank order (C's order): coalesced copies
     if (!(c_dbg & 1024)) {
-      for (int g = tid; g < ng; g += BS) {
-        const uint4 q = bm4[g];
-        if (q.x | q.y | q.z | q.w) {
-          int pos = gpre[g];
-          const unsigned wv[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            unsigned x = wv[j];
-            const int rb = lo + ((g * 4 + j) << 5) - 1;
-            while (x) {
-              out_ir[obase + pos++] = rb + __ffs(x);
-              x &= x - 1;
-            }
-          }
-        }
+      const int* rows = reinterpret_cast<const int*>(bm);
+      for (int j = tid; j < nout; j += BS) {
+        out_ir[obase + j] = rows[j];
+        st_emit(&out_val[obase + j], vals[j]);
       }
-      for (int j = tid; j < nout; j += BS) st_emit(&out_val[obase + j], vals[j]);
     }
     if ((c_dbg & 32) && tid == 0) {
       atomicAdd(&g_stat[10], (unsigned long long)total);
@@ -2931,8 +2977,8 @@ __global__ void k_col_records(const int32_t* __restrict__ perm, int n, const int
 
 template <int LOGT, int BS, int SR>
 static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B, const int2* cmap,
-                                  const cbg_tile& A, const float* valAf, const int64_t* colptr, cbg_tile& C,
-                                  hipStream_t s, DeferredFree& df) {
+                                  const int4* ainl, const cbg_tile& A, const float* valAf, const int64_t* colptr,
+                                  cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
   DBuf<SlabRec> rec(n);
   hipLaunchKernelGGL(k_col_records, dim3(nblk(n, 256)), dim3(256), 0, s, perm, n, B.cp, colptr, (int)A.m, rec.p);
@@ -2948,10 +2994,12 @@ static void launch_num_block_hash(const int32_t* perm, int n, const cbg_tile& B,
     // the main stream more CUs: 424 / 537 vs 418.5 ms at scale 22)
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, rec.p, n, queue.p, lm, B.ir, B.val, PMap{cmap, 0, 1},
-                       A.ir, valA, C.ir, C.val);
+                       A.ir, valA, C.ir, C.val, ainl);
   };
-  // A's f32 values (exact, see k_vals_f32) when the big-column path made them
-  if (valAf) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, float>, valAf);
+  // A's f32 values (exact, see k_vals_f32) when the big-column path made them;
+  // A's columns as inline records when the small-column passes have them
+  if (ainl) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, double, true>, A.val);
+  else if (valAf) go(k_num_slab_hash<SR, 1 << LOGT, BS, true, float>, valAf);
   else go(k_num_slab_hash<SR, 1 << LOGT, BS, true, double>, A.val);
   df.take(rec);
   df.take(queue);
@@ -2990,7 +3038,7 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
     const int per_cu = blocks_per_cu(k, BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
-                       A.ir, valA, C.ir, C.val);
+                       A.ir, valA, C.ir, C.val, (const int4*)nullptr);
   };
   // (A's exact f32 values come as (row, f32) records whenever they exist)
   if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp);
@@ -3195,7 +3243,7 @@ static int pick_panel_log(int64_t m) {
 
 template <int SR>
 static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* valAf, const cbg_tile& B,
-                             const int2* cmap, const int64_t* colptr, cbg_tile& C, const hipStream_t* sb,
+                             const int2* cmap, const int4* ainl, const int64_t* colptr, cbg_tile& C, const hipStream_t* sb,
                              DeferredFree& df) {
   const int32_t* P = nb.perm.p;
   auto at = [&](int b) { return P + nb.offset[b]; };
@@ -3203,10 +3251,10 @@ static void numeric_dispatch(const Binned& nb, const cbg_tile& A, const float* v
   launch_num_wave<7, SR>(at(2), nb.count[2], B, cmap, A, colptr, C, sb[2]);
   launch_num_wave<8, SR>(at(3), nb.count[3], B, cmap, A, colptr, C, sb[3]);
   launch_num_wave<9, SR>(at(4), nb.count[4], B, cmap, A, colptr, C, sb[4]);
-  launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, A, valAf, colptr, C, sb[5], df);
-  launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, A, valAf, colptr, C, sb[6], df);
-  launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, A, valAf, colptr, C, sb[7], df);
-  launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, A, valAf, colptr, C, sb[8], df);
+  launch_num_block_hash<10, 256, SR>(at(5), nb.count[5], B, cmap, ainl, A, valAf, colptr, C, sb[5], df);
+  launch_num_block_hash<11, 256, SR>(at(6), nb.count[6], B, cmap, ainl, A, valAf, colptr, C, sb[6], df);
+  launch_num_block_hash<12, 512, SR>(at(7), nb.count[7], B, cmap, ainl, A, valAf, colptr, C, sb[7], df);
+  launch_num_block_hash<13, 1024, SR>(at(8), nb.count[8], B, cmap, ainl, A, valAf, colptr, C, sb[8], df);
 }
 
 // Stream of each small-column bin: the big columns run on the main stream,
@@ -3760,10 +3808,17 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
                    thin_R ? (unsigned long long)sb.flops[THIN_BIN] : 0ull, ainl.p != nullptr);
     }
   }
-  if (thin_R && sb.count[THIN_BIN] > 0)
+  if (thin_R && sb.count[THIN_BIN] > 0) {
+    // on the copy stream (idle until the numeric), from the fork point, so the
+    // sort runs beside the small-column bins of both streams instead of behind
+    // the main stream's (its readback then waits for the sort alone)
+    CBG_HIP(hipStreamWaitEvent(scopy, ev_fork, 0));
     thin_columns(sb.perm.p + sb.offset[THIN_BIN], sb.count[THIN_BIN], thin_entries, (int64_t)sb.flops[THIN_BIN], A,
                  B, cmap.p, ainl.p, semiring, cnt.p, fused_slot.p, fused_ir.p, fused_val.p,
-                 (int64_t)fused_off[SYM_FUSED_LAST + 1], s, df);
+                 (int64_t)fused_off[SYM_FUSED_LAST + 1], scopy, df);
+    CBG_HIP(hipEventRecord(ev_cjoin, scopy));
+    CBG_HIP(hipStreamWaitEvent(s, ev_cjoin, 0));
+  }
   join(s);
   // Everything that depends only on the per-column counts is launched now and
   // read back in ONE synchronization: nnz(C) (column pointers), the number of
@@ -3929,8 +3984,11 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     // 3 rounds; round 3, before the copy stream: 9.9-10.2 vs 10.0 ms, off)
     balance_bins(nbn.flops, 1, 8, (double)nbn.flops[9], fused_w, nullptr, s, snum, numst, copy_stream);
   }
-  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
-  else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, colptr.p, C, numst, df);
+  // (the whole-column bins on the side stream overlap the slabs: serialized after
+  // them on the main stream they take ~13 ms per scale-22 step and the step is
+  // 1 ms longer, before them 0.6 ms longer -- profiles/r06_ab_numbins.json)
+  if (semiring == CBG_MIN_PLUS) numeric_dispatch<1>(nbn, A, bp.valAf, B, cmap.p, ainl.p, colptr.p, C, numst, df);
+  else numeric_dispatch<0>(nbn, A, bp.valAf, B, cmap.p, ainl.p, colptr.p, C, numst, df);
   if (fused && (fused_off[SYM_FUSED_LAST + 1] > 0 || (thin_R && sb.count[THIN_BIN] > 0)))
   {
     hipLaunchKernelGGL(k_copy_fused, dim3(nblk(nz, 256)), dim3(256), 0, sc, nz, fused_slot.p, cnt.p,
