@@ -345,6 +345,22 @@ struct Sem<1> {  // MinPlusSRing<double,double>: multiply = inf_plus (Semirings.
   static __device__ __forceinline__ double add(double a, double b) { return b < a ? b : a; }
 };
 
+// The same semirings accumulating exact integers in int32 LDS slots (IACC in
+// cbg_local.hip: every product an integer of magnitude < 2^31, which the f64
+// product v holds exactly)
+template <int SR>
+struct SemI;
+template <>
+struct SemI<0> {
+  static __device__ __forceinline__ int identity() { return 0; }
+  static __device__ __forceinline__ void lds_acc(int* p, double v) { atomicAdd(p, (int)v); }
+};
+template <>
+struct SemI<1> {
+  static __device__ __forceinline__ int identity() { return INT32_MAX; }
+  static __device__ __forceinline__ void lds_acc(int* p, double v) { atomicMin(p, (int)v); }
+};
+
 // In-LDS bitonic sort of N (power of two) (key,val) pairs by key, ascending,
 // by NT cooperating threads (tid in [0,NT)).  SYNC is a barrier functor.
 template <int N, int NT, class SYNC>

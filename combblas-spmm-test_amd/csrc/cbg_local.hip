@@ -1950,7 +1950,7 @@ __device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, cons
   }
 }
 
-template <int SR, int BS, typename VA>
+template <int SR, int BS, typename VA, bool IA>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
                                               const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                               int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
@@ -1968,14 +1968,19 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
           const int w = x.row >> 5;
           return RowVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.v};
         },
-        [&](const RowVal& x) { Sem<SR>::lds_acc(&vals[x.row], x.v); });
+        [&](const RowVal& x) {
+          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + x.row, x.v);
+          else Sem<SR>::lds_acc(&vals[x.row], x.v);
+        });
   }
 }
 
 // KEPT: every slab of the launch has its kept symbolic bitmap (the host saw
 // that no bitmap-mode pair went without a slot), so the kernel carries no
 // marking pass: 397.5-397.9 vs 403.0-404.4 ms at scale 22 (same box)
-template <int SR, int CAP, int BS, typename VA, bool KEPT>
+// IA: exact int32 accumulation (IACC, see k_int_bound): the value slots hold
+// int32 sums, stored to C as f64
+template <int SR, int CAP, int BS, typename VA, bool KEPT, bool IA>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_num_slab(const SlabRec* __restrict__ list, int n, int* __restrict__ queue,
                                                  int plog, const int32_t* __restrict__ irB,
                                                  const double* __restrict__ valB, PMap pm,
@@ -2072,7 +2077,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
       const int j = 4 * (k * BS + tid);
       if (j < words) *reinterpret_cast<uint4*>(bm + j) = have_bm ? pw[k] : make_uint4(0u, 0u, 0u, 0u);
     }
-    if (CBG_VEC_INIT) {  // 16-byte LDS stores (CAP is even, vals is 16-byte aligned)
+    if (IA) {
+      const int id = SemI<SR>::identity();
+      int4* v4 = reinterpret_cast<int4*>(vals);
+      for (int j = tid; j < (nout + 3) >> 2; j += BS) v4[j] = make_int4(id, id, id, id);
+    } else if (CBG_VEC_INIT) {  // 16-byte LDS stores (CAP is even, vals is 16-byte aligned)
       const double id = Sem<SR>::identity();
       double2* v2 = reinterpret_cast<double2*>(vals);
       for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
@@ -2179,7 +2188,7 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           total = pref[BS];
         }
         if ((c_dbg & 32) && pass == 1 && tid == 0) atomicAdd(&g_stat[4], (unsigned long long)total);
-        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, VA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, VA, IA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
       }
@@ -2203,9 +2212,11 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           x &= x - 1;
         }
       }
-      for (int j = tid; j < nout; j += BS) st_stream(&out_val[obase + j], vals[j]);
+      for (int j = tid; j < nout; j += BS)
+        st_stream(&out_val[obase + j], IA ? (double)reinterpret_cast<const int*>(vals)[j] : vals[j]);
     } else if (!(c_dbg & 8)) {
-      for (int j = tid; j < nout; j += BS) st_stream(&out_val[obase + j], vals[j]);
+      for (int j = tid; j < nout; j += BS)
+        st_stream(&out_val[obase + j], IA ? (double)reinterpret_cast<const int*>(vals)[j] : vals[j]);
       __syncthreads();
       int* rows = reinterpret_cast<int*>(vals);
       for (int w = tid; w < words; w += BS) {
@@ -2594,7 +2605,7 @@ static_assert(SPARSE_SLAB_MAX == 8 * RANK_BS, "segment scan: 8 products per thre
 __device__ __forceinline__ int popc4(const uint4& q) {
   return __popc(q.x) + __popc(q.y) + __popc(q.z) + __popc(q.w);
 }
-template <int SR, int NCAP, int BS, typename VA>
+template <int SR, int NCAP, int BS, typename VA, bool IA>
 __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict__ list, int n,
                                                       int* __restrict__ queue, const int32_t* __restrict__ irB,
                                                       const double* __restrict__ valB,
@@ -2693,9 +2704,15 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
     // 2. group ranks: thread t owns groups 4t .. 4t+3 (one 8-byte store of 4
     // u16); vals (aliasing the staging, now idle) set to the semiring's identity
     {
-      const double id = Sem<SR>::identity();
-      double2* v2 = reinterpret_cast<double2*>(vals);
-      for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
+      if (IA) {
+        const int id = SemI<SR>::identity();
+        int4* v4 = reinterpret_cast<int4*>(vals);
+        for (int j = tid; j < (nout + 3) >> 2; j += BS) v4[j] = make_int4(id, id, id, id);
+      } else {
+        const double id = Sem<SR>::identity();
+        double2* v2 = reinterpret_cast<double2*>(vals);
+        for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
+      }
       uint4 q[GPT];
       int sum = 0;
 #pragma unroll
@@ -2744,7 +2761,8 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
 #pragma unroll
       for (int k = 0; k < RK; ++k)
         if (rk[k] >= 0) {
-          Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
+          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk[k], xv[k]);
+          else Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
           rows[rk[k]] = lo + xr[k];
         }
     }
@@ -2756,7 +2774,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
       const int* rows = reinterpret_cast<const int*>(bm);
       for (int j = tid; j < nout; j += BS) {
         out_ir[obase + j] = rows[j];
-        st_emit(&out_val[obase + j], vals[j]);
+        st_emit(&out_val[obase + j], IA ? (double)reinterpret_cast<const int*>(vals)[j] : vals[j]);
       }
     }
     if ((c_dbg & 32) && tid == 0) {
@@ -3023,6 +3041,7 @@ struct BigPlan {
   const int* gbm_next = nullptr;  // kept-bitmap slots handed out (device), of gbm_slots
   int64_t gbm_slots = 0;
   bool all_kept = false;  // no bitmap-mode pair went without a slot (read with sync 3)
+  bool iacc = false;      // exact int32 accumulation (k_int_bound; read with sync 2)
 };
 
 
@@ -3060,12 +3079,15 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
                        A.ir, valA, C.ir, C.val, bp.gbm.p, bp.cuts.p);
   };
+  // (IACC only with the packed records: integers of magnitude <= 2^24 are f32-exact)
   if (bp.all_kept) {
-    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, double, true>, A.val);
+    if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, true, true>, bp.valAp);
+    else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true, false>, bp.valAp);
+    else go(k_num_slab<SR, CAP, BS, double, true, false>, A.val);
   } else {
-    if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, double, false>, A.val);
+    if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, false, true>, bp.valAp);
+    else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false, false>, bp.valAp);
+    else go(k_num_slab<SR, CAP, BS, double, false, false>, A.val);
   }
   df.take(queue);
 }
@@ -3084,8 +3106,9 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, B.ir, B.val, bp.pm(),
                        A.ir, valA, C.ir, C.val);
   };
-  if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV>, bp.valAp);
-  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double>, A.val);
+  if (bp.iacc) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, true>, bp.valAp);
+  else if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, false>, bp.valAp);
+  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double, false>, A.val);
   df.take(queue);
 }
 
@@ -3289,6 +3312,7 @@ struct APrep {
   int plog = -1;
   bool kmajor = false;  // cmapP's layout
   DBuf<float> valf;  // A's values as f32 (af == 1)
+  int ai = -1, amax = 0;  // A's values all integers of magnitude <= 2^24 (k_int_bound; -1: not checked), max |a|
   DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
@@ -3328,6 +3352,81 @@ __global__ void k_vals_f32(int64_t n, const double* __restrict__ v, float* __res
     }
   }
 }
+// Exact integer accumulation (IACC): when every value of A and B is an integer
+// of magnitude <= 2^24 (not -0.0) and every sum the slabs form is bounded below
+// 2^31 -- plus-times: max|A| max_j sum_k |B(k,j)| bounds |sum_k a_ik b_kj|;
+// min-plus: max|A| + max|B| -- the slab kernels accumulate in int32 LDS
+// atomics and store the sums as f64: every partial sum is an integer the f64
+// path also holds exactly, so C is the same, bit for bit, in any order.
+// k_int_bound: out[0] |= 1 if some value is not such an integer, out[1] =
+// max |value|; k_col_int_bound (a wave per column): the same and out[2] = the
+// largest column sum of |values| (capped at INT32_MAX).  (R-MAT scale 22: max
+// value 225, max column length 50,401, max column |sum| 79,824: the column-sum
+// bound is 1.8e7, the length bound 2.6e9 would fail.)
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int d = WAVE / 2; d > 0; d >>= 1) v = max(v, __shfl_xor(v, d, WAVE));
+  return v;
+}
+// the block's (flag, max, max) to out[0..2]: one set of atomics per block
+// (a wave each on three words serialized 2 M waves: 25 ms per scale-22 phase)
+__device__ __forceinline__ void block_int_bound_out(int bad, int mx, int cs, int* __restrict__ out) {
+  __shared__ int r[3];
+  if (threadIdx.x == 0) r[0] = r[1] = r[2] = 0;
+  __syncthreads();
+  const unsigned long long any = __ballot(bad);
+  mx = wave_max_i(mx);
+  cs = wave_max_i(cs);
+  if (lane_id() == 0) {
+    if (any) atomicOr(&r[0], 1);
+    atomicMax(&r[1], mx);
+    atomicMax(&r[2], cs);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (r[0]) atomicOr(&out[0], 1);
+    if (r[1]) atomicMax(&out[1], r[1]);
+    if (r[2]) atomicMax(&out[2], r[2]);
+  }
+}
+__device__ __forceinline__ bool int_value_bad(double x) {
+  const double ax = fabs(x);
+  return !(ax <= 16777216.0) || x != trunc(x) || (x == 0.0 && signbit(x));
+}
+__global__ __launch_bounds__(256) void k_int_bound(int64_t n, const double* __restrict__ v, int* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int bad = 0, mx = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double x = v[i];
+    if (int_value_bad(x)) bad = 1;
+    else mx = max(mx, (int)fabs(x));
+  }
+  block_int_bound_out(bad, mx, 0, out);
+}
+// a wave per column, grid-stride over the columns
+__global__ __launch_bounds__(256) void k_col_int_bound(int64_t nzc, const int64_t* __restrict__ cp,
+                                                       const double* __restrict__ v, int* __restrict__ out) {
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / WAVE);
+  int bad = 0, mx = 0, cs = 0;
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE; c < nzc; c += nw) {
+    double sum = 0.0;  // integers: exact below 2^53
+    for (int64_t q = cp[c] + lane_id(); q < cp[c + 1]; q += WAVE) {
+      const double x = v[q];
+      if (int_value_bad(x)) bad = 1;
+      else mx = max(mx, (int)fabs(x));
+      sum += fabs(x);
+    }
+#pragma unroll
+    for (int d = WAVE / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, WAVE);
+    cs = max(cs, sum < 2147483647.0 ? (int)sum : INT32_MAX);
+  }
+  block_int_bound_out(bad, mx, cs, out);
+}
+static bool iacc_bound_ok(int semiring, int amax, int bmax, int bcolsum) {
+  if (semiring == CBG_MIN_PLUS) return (int64_t)amax + bmax < (1LL << 30);
+  return (double)amax * (double)bcolsum < 2147483648.0;
+}
+
 // flops[0, nz) per B column and their total in flops[nz] (B.nnz > 0)
 static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned char* clen8, bool A_one_per_col,
                          int64_t* flops, hipStream_t s, DeferredFree& df) {
@@ -3364,6 +3463,7 @@ void aprep_end() {
   a.valf.release();
   a.valp.release();
   a.af = -1;
+  a.ai = -1;
   a.active = false;
   a.ir = a.cp = nullptr;
   a.ser_ir = a.ser_cp = 0;
@@ -3462,6 +3562,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.valf.release();
     ap.valp.release();
     ap.af = -1;
+    ap.ai = -1;
     ap.ir = A.ir;
     ap.cp = A.cp;
     ap.ser_ir = ser_ir;
@@ -3644,16 +3745,30 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<PackedRV> valp_own;
   DBuf<PackedRV>& valp = ap.active ? ap.valp : valp_own;
   int af = ap.active ? ap.af : -1, af_inexact = 0;
+  int ai = ap.active ? ap.ai : -1, amax = ap.active ? ap.amax : 0;
   DBuf<int> af_flag;
+  // [0] A not f32-exact | [1] A not integral, [2] max |a| | [4] B not integral,
+  // [5] max |b|, [6] B's largest column |sum| (IACC; read with sync 2)
+  int* afh = reinterpret_cast<int*>(host_stage(STAGE_AF));
   if (nbig > 0 && af < 0 && !sym_only) {
     valf.reset(A.nnz);
     valp.reset(A.nnz);
-    af_flag.reset(1);
-    CBG_HIP(hipMemsetAsync(af_flag.p, 0, sizeof(int), s));
+    af_flag.reset(4);  // ([3]: k_int_bound's unused column-sum slot)
+    CBG_HIP(hipMemsetAsync(af_flag.p, 0, 4 * sizeof(int), s));
     const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
     hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p, A.ir,
                        valp.p);
-    CBG_HIP(hipMemcpyAsync(host_stage(STAGE_AF), af_flag.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    hipLaunchKernelGGL(k_int_bound, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, af_flag.p + 1);
+    CBG_HIP(hipMemcpyAsync(afh, af_flag.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+  }
+  DBuf<int> bint;
+  afh[4] = 1;  // (no check: not integral)
+  if (nbig > 0 && !sym_only) {
+    bint.reset(3);
+    CBG_HIP(hipMemsetAsync(bint.p, 0, 3 * sizeof(int), s));
+    hipLaunchKernelGGL(k_col_int_bound, dim3((unsigned)std::min<int64_t>(nblk(B.nzc * WAVE, 256), (int64_t)device_cus() * 8)),
+                       dim3(256), 0, s, B.nzc, B.cp, B.val, bint.p);
+    CBG_HIP(hipMemcpyAsync(afh + 4, bint.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
   }
   if (nbig > 0) {
     // panel column maps of A (reused across phases like cmap)
@@ -3881,9 +3996,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     return;
   }
   if (af_flag.p) {
-    af_inexact = *reinterpret_cast<const int*>(host_stage(STAGE_AF));
+    af_inexact = afh[0];
     af = af_inexact ? 0 : 1;
-    if (ap.active) ap.af = af;
+    ai = afh[1] ? 0 : 1;
+    amax = afh[2];
+    if (ap.active) {
+      ap.af = af;
+      ap.ai = ai;
+      ap.amax = amax;
+    }
     if (!af) {
       valf.release();
       valp.release();
@@ -3891,6 +4012,8 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (af == 1) bp.valAf = valf.p;
   if (af == 1 && valp.p) bp.valAp = valp.p;
+  bp.iacc = bp.valAp && ai == 1 && !afh[4] && iacc_bound_ok(semiring, amax, afh[5], afh[6]);
+  work[CBG_WORK_IACC] = bp.iacc ? 1 : 0;
   {
     // test hook (CBG_FAULT_C_BYTES, read per call): C larger than this fails as
     // an out-of-memory would, after the symbolic pass -- the phase splitting of

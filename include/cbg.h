@@ -172,7 +172,9 @@ int cbg_last_stats(int64_t* flops, int64_t* nnz, double* ms_symbolic, double* ms
  * size 512 ... 8192, rank slabs of <= 1024 / 2048 / 4096 nonzeros), symbolic
  * (column, panel) units and panel-group units, group units run panel by panel,
  * columns of the one-pass small-column kernels, thin columns, entries of the
- * single-entry big columns, columns of the numeric hash / wave bins.
+ * single-entry big columns, columns of the numeric hash / wave bins, and the
+ * multiplies whose slab kernels accumulated exact integers in int32 (A's and B's
+ * values integers of magnitude <= 2^24 whose sums stay below 2^31).
  * counts[i] for i < min(n, CBG_WORK_N); returns CBG_WORK_N. */
 enum {
   CBG_WORK_BITMAP_SMALL_KEPT = 0,
@@ -189,7 +191,8 @@ enum {
   CBG_WORK_SINGLE_BIG_ENTRIES = 21,
   CBG_WORK_HASH_BIN_COLUMNS = 22,
   CBG_WORK_WAVE_BIN_COLUMNS = 23,
-  CBG_WORK_N = 24
+  CBG_WORK_IACC = 24, /* multiplies whose slabs accumulated exact integers in int32 */
+  CBG_WORK_N = 25
 };
 int cbg_last_work_stats(int64_t* counts, int n);
 /* last call's multiway merges (MergeAll / MultiwayMerge): partial entries in,

@@ -268,6 +268,42 @@ def test_slab_value_narrowing(cbg, kind):
             assert_tiles_equal(C.to_host(), ref)
 
 
+@pytest.mark.parametrize("kind", ["rmat", "negative", "scaled_past_bound", "minus_zero", "half_integer"])
+def test_int_accumulate_paths(cbg, kind):
+    """The slab kernels' exact int32 accumulation (IACC) runs when every value of A and
+    B is an integer of magnitude <= 2^24 (not -0.0) and max|A| max_j sum_k |B(k,j)|
+    < 2^31 (min-plus: max|A| + max|B| < 2^30), else the f64 path; either way C equals
+    the oracle's (integer sums are exact in f64 in any order).  R-MAT scale 14 (bitmap
+    and rank slabs), both semirings."""
+    Ah = cbg.rmat_tile(14, 16).to_host()
+    if kind == "negative":
+        Ah["val"] = -Ah["val"]
+    elif kind == "scaled_past_bound":
+        Ah["val"] = Ah["val"] * float(1 << 16)  # integers whose bound passes 2^31 (sums exact in f64)
+    elif kind == "minus_zero":
+        Ah["val"] = Ah["val"].copy()
+        Ah["val"][123] = -0.0
+    elif kind == "half_integer":
+        Ah["val"] = Ah["val"] + 0.5  # f32-exact, not integers
+    expect = {"rmat": True, "negative": True, "scaled_past_bound": False, "minus_zero": False,
+              "half_integer": False}[kind]
+    for sr in ("plus", "minplus"):
+        A = cbg.Tile.from_dict(Ah)
+        B = cbg.Tile.from_dict(Ah)
+        C = cbg.LocalHybridSpGEMM(A, B, sr)
+        w = cbg.last_work_stats()
+        assert w["bitmap_small_kept"] + w["bitmap_large_kept"] > 0, w
+        Ch = C.to_host()
+        for t in (A, B, C):
+            t.free()
+        on = w["int_accumulate"] > 0
+        if kind == "scaled_past_bound" and sr == "minplus":
+            assert on  # |a + b| stays far below 2^30
+        else:
+            assert on == expect, (kind, sr, w)
+        assert_tiles_equal(Ch, oracle_local(Ah, Ah, sr))  # exact: integer (or half-integer) sums
+
+
 def _panel_group_operands(m=(1 << 20) + 77):
     """Tall A (m = 2^20 + 77: 5 row panels of 2^18, the last one partial) and a B whose
     columns land in every big-column class: panel groups of 4 and 2 (expected products
