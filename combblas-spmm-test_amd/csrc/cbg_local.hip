@@ -3036,7 +3036,7 @@ struct BigPlan {
   DBuf<unsigned> gbm;       // kept symbolic bitmaps, slots of 2^(plog-5) words
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
   const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
-  const PackedRV* valAp = nullptr;  // ... and as (row, f32) records (CBG_APACK)
+  const PackedRV* valAp = nullptr;  // ... and as (row, f32) records
   DBuf<int> cuts, pcoff;  // multi-slab pairs' cut positions (sym_pair), per-pair offsets
   const int* gbm_next = nullptr;  // kept-bitmap slots handed out (device), of gbm_slots
   int64_t gbm_slots = 0;
@@ -3313,14 +3313,14 @@ struct APrep {
   bool kmajor = false;  // cmapP's layout
   DBuf<float> valf;  // A's values as f32 (af == 1)
   int ai = -1, amax = 0;  // A's values all integers of magnitude <= 2^24 (k_int_bound; -1: not checked), max |a|
-  DBuf<PackedRV> valp;  // (row, f32) records (af == 1, CBG_APACK)
+  DBuf<PackedRV> valp;  // (row, f32) records (af == 1)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
 
 // A's values narrowed to f32, and whether every one survives the round trip
 // exactly (NaN and values outside f32's range or precision do not).  When they
 // all do, the slab kernels read 4 B per product instead of 8 and widen them:
-// the products and sums are the f64 ones, bit for bit.  CBG_AF32=0 disables.
+// the products and sums are the f64 ones, bit for bit.
 // (stops early once some value is inexact: the copy is then not used --
 // GalerkinNew's A = L + D carries random diagonal values, and each of its
 // products checked all 68 M values for nothing: 0.21 ms)
@@ -3655,7 +3655,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     thin_entries = (int64_t)sp.big_entries[1];
   }
   // small-column symbolic bins on the side stream, big columns on the main one
-  // (bins 1-2 fused with their numeric unless CBG_FUSE_SMALL=0)
+  // (bins 1..SYM_FUSED_LAST fused with their numeric)
   DBuf<int32_t> fused_ir;
   DBuf<double> fused_val;
   DBuf<int64_t> fused_slot;  // temporary slot of each fused column (-1: none)
@@ -3691,7 +3691,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     for (int b = NSMALL; b < NSMALL + NGCLS; ++b) main_w += (double)sb.flops[b];
     double cost[NSMALL];
     for (int b = 0; b < NSMALL; ++b) cost[b] = (fused && b >= 1 && b <= SYM_FUSED_LAST) ? 2.0 : 1.0;
-    // Without CBG_SIDE: the small symbolic bins join the main stream, ahead of
+    // The small symbolic bins join the main stream, ahead of
     // the (column, panel) units, when those carry most of the flops over >= 8
     // row panels -- on the side stream they co-ran with k_sym_panel for its
     // whole length and slowed it (scale 22: 436.3 vs 443.1 ms, scale 24:
