@@ -359,6 +359,11 @@ struct alignas(8) PackedRV {
   int row;
   float v;
 };
+// (row, f64 value) records of A's entries for the f64-valued path: 12 bytes,
+// one dwordx3 gather per product instead of a row load and a value load
+struct alignas(4) PackedRVD {
+  int row, vlo, vhi;
+};
 
 // claim `row` in an LDS hash of mask + 1 slots (linear probing from h):
 // 1 if this call inserted it, 0 if it was there
@@ -1945,15 +1950,26 @@ __device__ __forceinline__ RowVal a_rowval(const int32_t* __restrict__ irA, cons
   if constexpr (std::is_same<VA, PackedRV>::value) {
     const PackedRV e = valA[q];
     return RowVal{e.row - lo, Sem<SR>::mul((double)e.v, b)};
+  } else if constexpr (std::is_same<VA, PackedRVD>::value) {
+    const PackedRVD e = valA[q];
+    return RowVal{e.row - lo, Sem<SR>::mul(__hiloint2double(e.vhi, e.vlo), b)};
   } else {
     return RowVal{irA[q] - lo, Sem<SR>::mul((double)valA[q], b)};
   }
 }
 
+struct RankVal {
+  int rank, row;
+  double v;
+};
+// IA: int32 sums in vals' first CAP ints, and each product's row written at its
+// rank into rows[] (the value region's second half; duplicates write the same
+// row), so the output copies the rows instead of walking the bitmap
 template <int SR, int BS, typename VA, bool IA>
 __device__ __forceinline__ void slab_products(int pass, int total, const int* pref, const int* st, const double* bv,
                                               const int32_t* __restrict__ irA, const VA* __restrict__ valA,
-                                              int lo, unsigned* bm, const unsigned short* wpre, double* vals) {
+                                              int lo, unsigned* bm, const unsigned short* wpre, double* vals,
+                                              int* rows) {
   if (pass == 0) {
     block_products<BS>(
         pref, total, [&](int sg) { return SegI{seg_off(st, pref, sg)}; },
@@ -1966,11 +1982,15 @@ __device__ __forceinline__ void slab_products(int pass, int total, const int* pr
         [&](const SegV& g, int u) { return a_rowval<SR>(irA, valA, g.off + u, g.b, lo); },
         [&](const RowVal& x) {
           const int w = x.row >> 5;
-          return RowVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.v};
+          return RankVal{(int)(wpre[w] + __popc(bm[w] & ((1u << (x.row & 31)) - 1u))), x.row, x.v};
         },
-        [&](const RowVal& x) {
-          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + x.row, x.v);
-          else Sem<SR>::lds_acc(&vals[x.row], x.v);
+        [&](const RankVal& x) {
+          if constexpr (IA) {
+            SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + x.rank, x.v);
+            rows[x.rank] = lo + x.row;
+          } else {
+            Sem<SR>::lds_acc(&vals[x.rank], x.v);
+          }
         });
   }
 }
@@ -2188,7 +2208,9 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
           total = pref[BS];
         }
         if ((c_dbg & 32) && pass == 1 && tid == 0) atomicAdd(&g_stat[4], (unsigned long long)total);
-        if (!(c_dbg & (2 << pass))) slab_products<SR, BS, VA, IA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals);
+        if (!(c_dbg & (2 << pass)))
+          slab_products<SR, BS, VA, IA>(pass, total, pref, st, bv, irA, valA, lo, bm, wpre, vals,
+                                        reinterpret_cast<int*>(vals) + CAP);
         __syncthreads();
         phase_mark(tmark, 4 + pass);
       }
@@ -2196,7 +2218,14 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(4))) void k_
     if (has_next) fetch_stage2(nrec);
     // values: coalesced copy; rows: each word scatters its set bits to their
     // ranks in LDS (reusing the value array), then a coalesced copy
-    if (!(c_dbg & 8) && CBG_ROWS_DIRECT) {
+    if (IA && !(c_dbg & 8)) {
+      // rows and values in rank order (C's order): coalesced copies
+      const int* ivals = reinterpret_cast<const int*>(vals);
+      for (int j = tid; j < nout; j += BS) {
+        out_ir[obase + j] = ivals[CAP + j];
+        st_stream(&out_val[obase + j], (double)ivals[j]);
+      }
+    } else if (!(c_dbg & 8) && CBG_ROWS_DIRECT) {
       // rows straight from the bitmap words to C (a wave's lanes hold
       // consecutive words, so their ranks -- the store addresses -- are
       // consecutive too): no LDS staging of the rows, no barriers
@@ -3037,6 +3066,7 @@ struct BigPlan {
   DBuf<int> gbm_slot;        // slot of a (column, panel) pair, -1 = none
   const float* valAf = nullptr;  // A's values as f32 when that is exact (slab kernels read 4 B, not 8)
   const PackedRV* valAp = nullptr;  // ... and as (row, f32) records
+  const PackedRVD* valAd = nullptr;  // A's (row, f64) records when its values are not f32-exact
   DBuf<int> cuts, pcoff;  // multi-slab pairs' cut positions (sym_pair), per-pair offsets
   const int* gbm_next = nullptr;  // kept-bitmap slots handed out (device), of gbm_slots
   int64_t gbm_slots = 0;
@@ -3061,7 +3091,7 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
   };
   // (A's exact f32 values come as (row, f32) records whenever they exist)
   if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp);
-  else go(k_num_slab_hash<SR, T, BS, false, double>, A.val);
+  else go(k_num_slab_hash<SR, T, BS, false, PackedRVD>, bp.valAd);
   df.take(queue);
 }
 
@@ -3083,11 +3113,11 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   if (bp.all_kept) {
     if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, true, true>, bp.valAp);
     else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true, false>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, double, true, false>, A.val);
+    else go(k_num_slab<SR, CAP, BS, PackedRVD, true, false>, bp.valAd);
   } else {
     if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, false, true>, bp.valAp);
     else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false, false>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, double, false, false>, A.val);
+    else go(k_num_slab<SR, CAP, BS, PackedRVD, false, false>, bp.valAd);
   }
   df.take(queue);
 }
@@ -3108,7 +3138,7 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
   };
   if (bp.iacc) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, true>, bp.valAp);
   else if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, false>, bp.valAp);
-  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double, false>, A.val);
+  else go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRVD, false>, bp.valAd);
   df.take(queue);
 }
 
@@ -3314,6 +3344,7 @@ struct APrep {
   DBuf<float> valf;  // A's values as f32 (af == 1)
   int ai = -1, amax = 0;  // A's values all integers of magnitude <= 2^24 (k_int_bound; -1: not checked), max |a|
   DBuf<PackedRV> valp;  // (row, f32) records (af == 1)
+  DBuf<PackedRVD> valpd;  // (row, f64) records (af == 0)
   int af = -1;       // -1 not checked yet, 0 some value is not an exact f32, 1 valf holds A's values
 };
 
@@ -3427,6 +3458,15 @@ static bool iacc_bound_ok(int semiring, int amax, int bmax, int bcolsum) {
   return (double)amax * (double)bcolsum < 2147483648.0;
 }
 
+// A's (row, f64) records for the f64-valued slab path
+__global__ void k_pack_rvd(int64_t n, const int32_t* __restrict__ ir, const double* __restrict__ v,
+                           PackedRVD* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long b = __double_as_longlong(v[i]);
+    out[i] = PackedRVD{ir[i], (int)b, (int)(b >> 32)};
+  }
+}
+
 // flops[0, nz) per B column and their total in flops[nz] (B.nnz > 0)
 static void launch_flops(const cbg_tile& B, const int2* cmap, const unsigned char* clen8, bool A_one_per_col,
                          int64_t* flops, hipStream_t s, DeferredFree& df) {
@@ -3462,6 +3502,7 @@ void aprep_end() {
   a.cmapP.release();
   a.valf.release();
   a.valp.release();
+  a.valpd.release();
   a.af = -1;
   a.ai = -1;
   a.active = false;
@@ -3561,6 +3602,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     ap.cmapP.release();
     ap.valf.release();
     ap.valp.release();
+    ap.valpd.release();
     ap.af = -1;
     ap.ai = -1;
     ap.ir = A.ir;
@@ -3744,6 +3786,7 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   DBuf<float>& valf = ap.active ? ap.valf : valf_own;
   DBuf<PackedRV> valp_own;
   DBuf<PackedRV>& valp = ap.active ? ap.valp : valp_own;
+  DBuf<PackedRVD> valpd_own;
   int af = ap.active ? ap.af : -1, af_inexact = 0;
   int ai = ap.active ? ap.ai : -1, amax = ap.active ? ap.amax : 0;
   DBuf<int> af_flag;
@@ -4012,6 +4055,16 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (af == 1) bp.valAf = valf.p;
   if (af == 1 && valp.p) bp.valAp = valp.p;
+  if (af == 0 && nbig > 0) {
+    // the f64-valued slab path reads A as (row, f64) records (built once per A)
+    DBuf<PackedRVD>& vd = ap.active ? ap.valpd : valpd_own;
+    if (!vd.p) {
+      vd.reset(A.nnz);
+      hipLaunchKernelGGL(k_pack_rvd, dim3((unsigned)std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16)),
+                         dim3(256), 0, s, A.nnz, A.ir, A.val, vd.p);
+    }
+    bp.valAd = vd.p;
+  }
   bp.iacc = bp.valAp && ai == 1 && !afh[4] && iacc_bound_ok(semiring, amax, afh[5], afh[6]);
   work[CBG_WORK_IACC] = bp.iacc ? 1 : 0;
   {
