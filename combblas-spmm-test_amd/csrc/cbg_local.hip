@@ -3089,9 +3089,11 @@ static void launch_slab_hash(const SlabRec* list, int n, const BigPlan& bp, cons
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
                        A.ir, valA, C.ir, C.val, (const int4*)nullptr);
   };
-  // (A's exact f32 values come as (row, f32) records whenever they exist)
+  // (A's exact f32 values come as (row, f32) records whenever they exist; f64
+  // values as (row, f64) records when they were worth packing, see k_pack_rvd)
   if (bp.valAp) go(k_num_slab_hash<SR, T, BS, false, PackedRV>, bp.valAp);
-  else go(k_num_slab_hash<SR, T, BS, false, PackedRVD>, bp.valAd);
+  else if (bp.valAd) go(k_num_slab_hash<SR, T, BS, false, PackedRVD>, bp.valAd);
+  else go(k_num_slab_hash<SR, T, BS, false, double>, A.val);
   df.take(queue);
 }
 
@@ -3113,11 +3115,13 @@ static void launch_slab_bitmap(const SlabRec* list, int n, const BigPlan& bp, co
   if (bp.all_kept) {
     if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, true, true>, bp.valAp);
     else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, true, false>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, PackedRVD, true, false>, bp.valAd);
+    else if (bp.valAd) go(k_num_slab<SR, CAP, BS, PackedRVD, true, false>, bp.valAd);
+    else go(k_num_slab<SR, CAP, BS, double, true, false>, A.val);
   } else {
     if (bp.iacc) go(k_num_slab<SR, CAP, BS, PackedRV, false, true>, bp.valAp);
     else if (bp.valAp) go(k_num_slab<SR, CAP, BS, PackedRV, false, false>, bp.valAp);
-    else go(k_num_slab<SR, CAP, BS, PackedRVD, false, false>, bp.valAd);
+    else if (bp.valAd) go(k_num_slab<SR, CAP, BS, PackedRVD, false, false>, bp.valAd);
+    else go(k_num_slab<SR, CAP, BS, double, false, false>, A.val);
   }
   df.take(queue);
 }
@@ -3138,7 +3142,8 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
   };
   if (bp.iacc) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, true>, bp.valAp);
   else if (bp.valAp) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRV, false>, bp.valAp);
-  else go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRVD, false>, bp.valAd);
+  else if (bp.valAd) go(k_num_slab_rank<SR, NCAP, RANK_BS, PackedRVD, false>, bp.valAd);
+  else go(k_num_slab_rank<SR, NCAP, RANK_BS, double, false>, A.val);
   df.take(queue);
 }
 
@@ -3424,19 +3429,39 @@ __device__ __forceinline__ bool int_value_bad(double x) {
   const double ax = fabs(x);
   return !(ax <= 16777216.0) || x != trunc(x) || (x == 0.0 && signbit(x));
 }
-__global__ __launch_bounds__(256) void k_int_bound(int64_t n, const double* __restrict__ v, int* __restrict__ out) {
+// fail fast: a wave that sees a bad value raises out[0] at once (one store per
+// wave), and every wave stops at its next check once it is up; k_int_bound
+// does nothing when k_vals_f32 (before it on the stream) found A not
+// f32-exact (skip[0]), k_col_int_bound nothing when A is not integral (skip:
+// A's flags, in this call; the host skips the launch for a cached verdict)
+// (GalerkinNew scale 22, f64 values: the two checks read 0.47 ms for nothing)
+__device__ __forceinline__ bool int_bound_raise(int bad, int* __restrict__ out) {
+  const unsigned long long any = __ballot(bad);
+  if (any && lane_id() == __ffsll((long long)any) - 1 && !*reinterpret_cast<volatile int*>(out))
+    *reinterpret_cast<volatile int*>(out) = 1;
+  return any || *reinterpret_cast<volatile int*>(out);
+}
+__global__ __launch_bounds__(256) void k_int_bound(int64_t n, const double* __restrict__ v, int* __restrict__ out,
+                                                   const int* __restrict__ skip) {
+  if (*skip) return;  // (uniform: written by an earlier kernel)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int bad = 0, mx = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double x = v[i];
-    if (int_value_bad(x)) bad = 1;
-    else mx = max(mx, (int)fabs(x));
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x; i0 < n; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    if (i < n) {
+      const double x = v[i];
+      if (int_value_bad(x)) bad = 1;
+      else mx = max(mx, (int)fabs(x));
+    }
+    if (int_bound_raise(bad, out)) break;
   }
   block_int_bound_out(bad, mx, 0, out);
 }
 // a wave per column, grid-stride over the columns
 __global__ __launch_bounds__(256) void k_col_int_bound(int64_t nzc, const int64_t* __restrict__ cp,
-                                                       const double* __restrict__ v, int* __restrict__ out) {
+                                                       const double* __restrict__ v, int* __restrict__ out,
+                                                       const int* __restrict__ skip) {
+  if (skip && (skip[0] | skip[1])) return;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x / WAVE);
   int bad = 0, mx = 0, cs = 0;
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / WAVE; c < nzc; c += nw) {
@@ -3450,6 +3475,7 @@ __global__ __launch_bounds__(256) void k_col_int_bound(int64_t nzc, const int64_
 #pragma unroll
     for (int d = WAVE / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, WAVE);
     cs = max(cs, sum < 2147483647.0 ? (int)sum : INT32_MAX);
+    if (int_bound_raise(bad, out)) break;
   }
   block_int_bound_out(bad, mx, cs, out);
 }
@@ -3801,16 +3827,16 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     const int64_t nb = std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16);
     hipLaunchKernelGGL(k_vals_f32, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, valf.p, af_flag.p, A.ir,
                        valp.p);
-    hipLaunchKernelGGL(k_int_bound, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, af_flag.p + 1);
+    hipLaunchKernelGGL(k_int_bound, dim3((unsigned)nb), dim3(256), 0, s, A.nnz, A.val, af_flag.p + 1, af_flag.p);
     CBG_HIP(hipMemcpyAsync(afh, af_flag.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
   }
   DBuf<int> bint;
   afh[4] = 1;  // (no check: not integral)
-  if (nbig > 0 && !sym_only) {
+  if (nbig > 0 && !sym_only && af != 0 && ai != 0) {
     bint.reset(3);
     CBG_HIP(hipMemsetAsync(bint.p, 0, 3 * sizeof(int), s));
     hipLaunchKernelGGL(k_col_int_bound, dim3((unsigned)std::min<int64_t>(nblk(B.nzc * WAVE, 256), (int64_t)device_cus() * 8)),
-                       dim3(256), 0, s, B.nzc, B.cp, B.val, bint.p);
+                       dim3(256), 0, s, B.nzc, B.cp, B.val, bint.p, af_flag.p);
     CBG_HIP(hipMemcpyAsync(afh + 4, bint.p, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
   }
   if (nbig > 0) {
@@ -4055,9 +4081,13 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
   }
   if (af == 1) bp.valAf = valf.p;
   if (af == 1 && valp.p) bp.valAp = valp.p;
-  if (af == 0 && nbig > 0) {
-    // the f64-valued slab path reads A as (row, f64) records (built once per A)
-    DBuf<PackedRVD>& vd = ap.active ? ap.valpd : valpd_own;
+  uint64_t big_fl = 0;
+  for (int b = NSMALL; b < NSMALL + NGCLS; ++b) big_fl += sb.flops[b];
+  DBuf<PackedRVD>& vd = ap.active ? ap.valpd : valpd_own;
+  if (af == 0 && nbig > 0 && (vd.p || big_fl >= 4 * (uint64_t)A.nnz)) {
+    // the f64-valued slab path reads A as (row, f64) records (built once per A,
+    // when the big columns' products are enough to pay for its 24 B per entry:
+    // GalerkinNew scale 22 packed 68 M entries, 0.34 ms, for 3.7 M products)
     if (!vd.p) {
       vd.reset(A.nnz);
       hipLaunchKernelGGL(k_pack_rvd, dim3((unsigned)std::min<int64_t>(nblk(A.nnz, 256), (int64_t)device_cus() * 16)),
