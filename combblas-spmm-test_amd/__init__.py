@@ -403,7 +403,8 @@ WORK_CLASSES = (["bitmap_small_kept", "bitmap_small_mark", "bitmap_large_kept", 
                 ["hash_T%d" % t for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)] +
                 ["rank_N%d" % n for n in (1024, 2048, 4096)] +
                 ["sym_panel_units", "sym_group_units", "sym_deferred_units", "esc_columns", "thin_columns",
-                 "single_big_entries", "hash_bin_columns", "wave_bin_columns", "int_accumulate"])
+                 "single_big_entries", "hash_bin_columns", "wave_bin_columns", "int_accumulate"] +
+                ["group_rank_N%d" % n for n in (2048, 4096)])
 
 
 def last_work_stats():

@@ -1304,13 +1304,21 @@ constexpr int SLAB_RANK_NCLS = 3;
 static_assert(CBG_WORK_RANK0 - CBG_WORK_HASH0 == SLAB_HASH_NCLS && CBG_WORK_SYM_PANEL_UNITS - CBG_WORK_RANK0 == SLAB_RANK_NCLS,
               "cbg_last_work_stats classes");
 constexpr int SLAB_RANK0 = 2 + SLAB_HASH_NCLS;
-constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS + SLAB_RANK_NCLS;
-__device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank_span, int rank_min) {
+// + group rank slabs (k_num_slab_grank) of <= 2048 / 4096 nonzeros: the
+// panel-group slabs of more than grank_min nonzeros spanning <= 2^22 rows
+constexpr int SLAB_GRANK_NCLS = 2;
+constexpr int SLAB_GRANK0 = SLAB_RANK0 + SLAB_RANK_NCLS;
+static_assert(CBG_WORK_GRANK0 == CBG_WORK_IACC + 1 && CBG_WORK_N == CBG_WORK_GRANK0 + SLAB_GRANK_NCLS,
+              "cbg_last_work_stats group rank classes");
+constexpr int SLAB_NCLS = 2 + SLAB_HASH_NCLS + SLAB_RANK_NCLS + SLAB_GRANK_NCLS;
+__device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank_span, int rank_min, int grank_min) {
   const int w = d.w;
   if (w & SLAB_SPARSE) {
     const int c = w & SLAB_CNT_MASK;
     if (c > rank_min && rank_span > 0 && d.y - d.x <= rank_span)
       return SLAB_RANK0 + (c <= 1024 ? 0 : c <= 2048 ? 1 : 2);
+    if (c > grank_min && d.y - d.x > rank_span && d.y - d.x <= (1 << 22))
+      return SLAB_GRANK0 + (c <= 2048 ? 0 : 1);
     int k = 0;
     while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
     return 2 + k;
@@ -1327,7 +1335,7 @@ __host__ __device__ inline int slab_kr(int R) { return SLAB_NCLS * R <= SLAB_KEY
 // pass 1: within-panel -> within-column offsets, (class, panel) counts
 __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab, const int32_t* __restrict__ cnt_br,
                              int4* __restrict__ desc, int small_cap, int rank_span, int rank_min,
-                             int* __restrict__ counts) {
+                             int grank_min, int* __restrict__ counts) {
   extern __shared__ int lc[];  // [SLAB_NCLS * KR]
   const int KR = slab_kr(R), NK = SLAB_NCLS * KR;
   for (int k = threadIdx.x; k < NK; k += blockDim.x) lc[k] = 0;
@@ -1340,7 +1348,7 @@ __global__ void k_slab_count(int nbig, int R, const int32_t* __restrict__ nslab,
       for (int s = 0; s < nslab[br]; ++s) {
         int4& d = desc[(int64_t)br * NFINE_MAX + s];
         d.z += off;
-        atomicAdd(&lc[slab_class(d, small_cap, rank_span, rank_min) * KR + (KR > 1 ? r : 0)], 1);
+        atomicAdd(&lc[slab_class(d, small_cap, rank_span, rank_min, grank_min) * KR + (KR > 1 ? r : 0)], 1);
       }
       off += cnt_br[br];
     }
@@ -1367,7 +1375,7 @@ __global__ void k_slab_bases(int R, const int* __restrict__ counts, int* __restr
 }
 // pass 2: slab records into their (class, panel) segment of one list
 __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, const int4* __restrict__ desc,
-                            int small_cap, int rank_span, int rank_min, int* __restrict__ cursor,
+                            int small_cap, int rank_span, int rank_min, int grank_min, int* __restrict__ cursor,
                             SlabRec* __restrict__ list,
                             const int32_t* __restrict__ perm_big, const int64_t* __restrict__ cpB,
                             const int64_t* __restrict__ colptr, const int* __restrict__ gbm_slot, int plog,
@@ -1383,7 +1391,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
     for (int r = 0; r < R; ++r) {
       const int br = b * R + r;
       for (int s = 0; s < nslab[br]; ++s)
-        atomicAdd(&lc[slab_class(desc[(int64_t)br * NFINE_MAX + s], small_cap, rank_span, rank_min) * KR +
+        atomicAdd(&lc[slab_class(desc[(int64_t)br * NFINE_MAX + s], small_cap, rank_span, rank_min, grank_min) * KR +
                       (KR > 1 ? r : 0)],
                   1);
     }
@@ -1402,7 +1410,7 @@ __global__ void k_slab_fill(int nbig, int R, const int32_t* __restrict__ nslab, 
     const int R1 = (int)min((int64_t)R0 + (1LL << plog), m_rows);
     for (int s = 0; s < nslab[br]; ++s) {
       const int4 d = desc[(int64_t)br * NFINE_MAX + s];
-      const int key = slab_class(d, small_cap, rank_span, rank_min) * KR + (KR > 1 ? r : 0);
+      const int key = slab_class(d, small_cap, rank_span, rank_min, grank_min) * KR + (KR > 1 ? r : 0);
       SlabRec rec;
       rec.obase = cbase + d.z;
       rec.p0 = p0;
@@ -2313,6 +2321,15 @@ __device__ __forceinline__ void build_segids(unsigned short* seg16, int* tmp) {
         h[j + 2 * k + 1] = (int)(v[k] >> 16);
       }
     }
+  } else if constexpr (E % 4 == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 4) {
+      const uint2 q = reinterpret_cast<const uint2*>(seg16 + tid * E + j)[0];
+      h[j] = (int)(q.x & 0xffffu);
+      h[j + 1] = (int)(q.x >> 16);
+      h[j + 2] = (int)(q.y & 0xffffu);
+      h[j + 3] = (int)(q.y >> 16);
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < E; ++j) h[j] = seg16[tid * E + j];
@@ -2342,6 +2359,11 @@ __device__ __forceinline__ void build_segids(unsigned short* seg16, int* tmp) {
       for (int k = 0; k < 4; ++k) v[k] = (unsigned)h[j + 2 * k] | ((unsigned)h[j + 2 * k + 1] << 16);
       reinterpret_cast<uint4*>(seg16 + tid * E + j)[0] = make_uint4(v[0], v[1], v[2], v[3]);
     }
+  } else if constexpr (E % 4 == 0) {
+#pragma unroll
+    for (int j = 0; j < E; j += 4)
+      reinterpret_cast<uint2*>(seg16 + tid * E + j)[0] =
+          make_uint2((unsigned)h[j] | ((unsigned)h[j + 1] << 16), (unsigned)h[j + 2] | ((unsigned)h[j + 3] << 16));
   } else {
 #pragma unroll
     for (int j = 0; j < E; ++j) seg16[tid * E + j] = (unsigned short)h[j];
@@ -2624,6 +2646,14 @@ struct SlabRankLds {
   static_assert(SEG_BYTES % 16 == 0 && BM_OFF % 16 == 0 && GPRE_OFF % 16 == 0, "rank slab LDS alignment");
 };
 constexpr int RANK_BS = 512;
+// group rank slabs (k_num_slab_grank): spans <= 2^22 rows (level 1: a bit per
+// 32 rows, <= 4096 words), <= GRANK_PMAX products (>= sym_group's 2/3 of GROUP_T)
+constexpr int GRANK_SPAN_LOG = 22;
+constexpr int GRANK_L1W = 1 << (GRANK_SPAN_LOG - 10);
+constexpr int GRANK_PMAX = 6144;
+static_assert((SLAB_WORDS > GROUP_T ? SLAB_WORDS : GROUP_T) * CBG_SYM_LOAD_DEN <= GRANK_PMAX * CBG_SYM_LOAD_NUM,
+              "a panel group's products (sym_group: table <= hwords at load NUM/DEN) fit a group rank slab");
+static_assert(SPARSE_NNZ_MAX <= 4096 && BIG_BS <= RANK_BS, "group rank slab: nonzeros and B entries");
 static_assert(4096 <= SLAB_WORDS, "a rank slab's rows (<= 4096) are written into its bitmap's words");
 // a rank slab stages one B entry per thread: the symbolic's sparse pairs (the
 // rank slabs' source, sym_pair) have <= BIG_BS B entries
@@ -2811,6 +2841,247 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
       atomicAdd(&g_stat[11], (unsigned long long)nout);
     }
     __syncthreads();  // LDS is reset for the next slab
+    phase_mark(tmark, 20);
+    if (!has_next) break;
+    i = inext;
+    rec = nrec;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// numeric of a panel-group hash slab by two-level rank: no hash, no sort
+// ----------------------------------------------------------------------------
+// A panel group's slab (sym_group: <= BIG_BS B entries, <= GROUP_T * 2/3
+// products, <= SPARSE_NNZ_MAX nonzeros) spans up to 2^22 rows, too many for the
+// rank slab's one-bit-per-row bitmap (32 KiB per 2^18 rows).  Its rows are
+// sparse, so the bitmap is split in two levels:
+//   1. level 1, a bit per 32-row block of the span (<= 2^17 bits, 16 KiB):
+//      every product marks its block (ds_or); a scan of the popcounts gives
+//      every touched block its slot, in row order (slots <= nonzeros);
+//   2. level 2, a word per slot: every product marks its row's bit in its
+//      block's word (ds_or); a scan of those popcounts gives every slot its
+//      first rank;
+//   3. a product's rank = its slot's rank + the bits below it in the word;
+//      the products accumulate at their ranks and write their rows at them
+//      (into level 1's words, idle by then): C's rows and values come out in
+//      order with coalesced copies.
+// Against the hash slab (a returning CAS chain per product, then a bucket
+// counting sort of the table) this is two ds_or, two lookups and the
+// semiring's atomic per product.
+template <int NCAP, int BS>
+struct SlabGRankLds {
+  // ust: seg16[GRANK_PMAX] u16 | srec[BS]; from step 2 on vals[NCAP]
+  // l1[GRANK_L1W] (level 1; then C's rows) | g1pre[GRANK_L1W/4] u16 |
+  // l2[NCAP] | g2pre[NCAP/4] u16 | tmp[BS/64+4]
+  static constexpr int SEG_BYTES = GRANK_PMAX * 2;
+  static constexpr int UST = NCAP * 8 > SEG_BYTES + BS * 16 ? NCAP * 8 : SEG_BYTES + BS * 16;
+  static constexpr int L1_OFF = UST;
+  static constexpr int G1_OFF = L1_OFF + GRANK_L1W * 4;
+  static constexpr int L2_OFF = G1_OFF + (GRANK_L1W / 4) * 2;
+  static constexpr int G2_OFF = L2_OFF + NCAP * 4;
+  static constexpr int TMP_OFF = G2_OFF + (NCAP / 4) * 2;
+  static constexpr int BYTES = TMP_OFF + (BS / WAVE + 4) * 4;
+  static_assert(SEG_BYTES % 16 == 0 && L1_OFF % 16 == 0 && G1_OFF % 16 == 0 && L2_OFF % 16 == 0 &&
+                    G2_OFF % 16 == 0 && TMP_OFF % 16 == 0,
+                "group rank slab LDS alignment");
+  static_assert(NCAP <= GRANK_L1W, "a slab's rows (<= NCAP) are written into level 1's words");
+};
+// the rank of bit b of a bitmap: its 4-word group's rank + the bits below it
+__device__ __forceinline__ int bitmap_rank(const uint4* bm4, const unsigned short* gpre, int b) {
+  const int wd = b >> 5, g = wd >> 2, j = wd & 3;
+  const uint4 q = bm4[g];
+  const unsigned below = (1u << (b & 31)) - 1u;
+  int x = gpre[g];
+  x += j > 0 ? __popc(q.x) : __popc(q.x & below);
+  if (j >= 1) x += j > 1 ? __popc(q.y) : __popc(q.y & below);
+  if (j >= 2) x += j > 2 ? __popc(q.z) : __popc(q.z & below);
+  if (j >= 3) x += __popc(q.w & below);
+  return x;
+}
+// the first rank of every 4-word group of bm4[0, ng) into gpre (u16, GPT groups
+// per thread, GPT even); returns the total (block-uniform)
+template <int BS, int GPT>
+__device__ __forceinline__ int bitmap_group_ranks(const uint4* bm4, int ng, unsigned short* gpre, int* tmp) {
+  const int tid = threadIdx.x;
+  uint4 q[GPT];
+  int sum = 0;
+#pragma unroll
+  for (int j = 0; j < GPT; ++j) {
+    const int g = tid * GPT + j;
+    q[j] = g < ng ? bm4[g] : make_uint4(0u, 0u, 0u, 0u);
+    sum += popc4(q[j]);
+  }
+  int tot;
+  int run = block_excl_scan<BS>(sum, tmp, &tot);
+  unsigned pk[GPT / 2];
+#pragma unroll
+  for (int j = 0; j < GPT; j += 2) {
+    const unsigned a = (unsigned)run;
+    run += popc4(q[j]);
+    pk[j / 2] = a | ((unsigned)run << 16);
+    run += popc4(q[j + 1]);
+  }
+  if (tid * GPT < ng) {
+    if constexpr (GPT == 2) *reinterpret_cast<unsigned*>(gpre + tid * GPT) = pk[0];
+    else if constexpr (GPT == 4) *reinterpret_cast<uint2*>(gpre + tid * GPT) = make_uint2(pk[0], pk[1]);
+    else {
+#pragma unroll
+      for (int j = 0; j < GPT / 2; ++j) reinterpret_cast<unsigned*>(gpre + tid * GPT)[j] = pk[j];
+    }
+  }
+  return tot;
+}
+template <int SR, int NCAP, int BS, typename VA, bool IA>
+__global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict__ list, int n,
+                                                       int* __restrict__ queue, int plog,
+                                                       const int32_t* __restrict__ irB,
+                                                       const double* __restrict__ valB, PMap pm,
+                                                       const int32_t* __restrict__ irA, const VA* __restrict__ valA,
+                                                       int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
+  using L = SlabGRankLds<NCAP, BS>;
+  constexpr int NW = BS / WAVE;
+  constexpr int RK = GRANK_PMAX / BS;        // products per thread
+  constexpr int G1PT = (GRANK_L1W / 4) / BS;  // level-1 groups per thread in its scan
+  constexpr int G2PT = (NCAP / 4 + BS - 1) / BS < 2 ? 2 : (NCAP / 4 + BS - 1) / BS;
+  static_assert(G1PT >= 2 && G1PT % 2 == 0 && G2PT % 2 == 0, "group rank scans: pairs of u16 ranks");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* vals = reinterpret_cast<double*>(smem);
+  unsigned short* seg16 = reinterpret_cast<unsigned short*>(smem);
+  SegRec* srec = reinterpret_cast<SegRec*>(smem + L::SEG_BYTES);
+  unsigned* l1 = reinterpret_cast<unsigned*>(smem + L::L1_OFF);
+  uint4* l1q = reinterpret_cast<uint4*>(smem + L::L1_OFF);
+  unsigned short* g1pre = reinterpret_cast<unsigned short*>(smem + L::G1_OFF);
+  unsigned* l2 = reinterpret_cast<unsigned*>(smem + L::L2_OFF);
+  uint4* l2q = reinterpret_cast<uint4*>(smem + L::L2_OFF);
+  unsigned short* g2pre = reinterpret_cast<unsigned short*>(smem + L::G2_OFF);
+  int* tmp = reinterpret_cast<int*>(smem + L::TMP_OFF);
+  const int tid = threadIdx.x;
+  int i = blockIdx.x;
+  if (i >= n) return;
+  int p_ir = 0;
+  double p_bv = 0.0;
+  int2 p_ce = make_int2(0, 0);
+  auto fetch1 = [&](const SlabRec& r) {
+    if (tid < r.nb) {
+      p_ir = irB[r.p0 + tid];
+      p_bv = valB[r.p0 + tid];
+    }
+  };
+  // A(:,k)'s run over the group's panels r .. r1: the first panel's start to
+  // the last one's end
+  auto fetch2 = [&](const SlabRec& r) {
+    if (tid < r.nb) p_ce = make_int2(pm.at(r.r, p_ir).x, pm.at((r.hi - 1) >> plog, p_ir).y);
+  };
+  SlabRec rec = list[i];
+  int qnext = 0;
+  if (tid == 0) qnext = (int)gridDim.x + atomicAdd(queue, 1);
+  fetch1(rec);
+  fetch2(rec);
+  while (true) {
+    if (tid == 0) {
+      tmp[NW + 2] = qnext;
+      qnext = (int)gridDim.x + atomicAdd(queue, 1);
+    }
+    unsigned long long tmark = wall_clock64();
+    const int lo = rec.lo, nout = rec.nout;
+    const int ng1 = (((rec.hi - lo + 1023) >> 10) + 3) >> 2;  // level-1 groups (32 rows a bit, 32 bits a word)
+    const int64_t obase = rec.obase;
+    for (int g = tid; g < ng1; g += BS) l1q[g] = make_uint4(0u, 0u, 0u, 0u);
+    for (int g = tid; g < (nout + 3) >> 2; g += BS) l2q[g] = make_uint4(0u, 0u, 0u, 0u);
+    for (int g = tid; g < GRANK_PMAX / 8; g += BS) reinterpret_cast<uint4*>(seg16)[g] = make_uint4(0u, 0u, 0u, 0u);
+    const int len = tid < rec.nb ? p_ce.y - p_ce.x : 0;
+    int total;
+    const int ex = block_excl_scan<BS>(len, tmp, &total);  // (its barriers order the zeroing above)
+    srec[tid] = SegRec{(tid < rec.nb ? p_ce.x : 0) - ex, 0, tid < rec.nb ? p_bv : 0.0};
+    if (len > 0) seg16[ex] = (unsigned short)tid;
+    const int inext = tmp[NW + 2];
+    const bool has_next = inext < n;
+    SlabRec nrec;
+    if (has_next) nrec = list[inext];
+    __syncthreads();
+    build_segids<BS, RK>(seg16, tmp);
+    phase_mark(tmark, 16);
+    // 1. products into registers, their 32-row blocks marked in level 1
+    int xr[RK];
+    double xv[RK];
+    {
+      int sg[RK];
+#pragma unroll
+      for (int k = 0; k < RK; ++k) {
+        const int u = tid + k * BS;
+        sg[k] = u < total ? seg16[u] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < RK; ++k) {
+        xr[k] = -1;
+        if (sg[k] >= 0) {
+          const SegRec r = srec[sg[k]];
+          const RowVal x = a_rowval<SR, VA>(irA, valA, r.off + tid + k * BS, r.b, lo);
+          xr[k] = x.row;
+          xv[k] = x.v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < RK; ++k)
+        if (xr[k] >= 0) atomicOr(&l1[xr[k] >> 10], 1u << ((xr[k] >> 5) & 31));
+    }
+    if (has_next) fetch1(nrec);
+    __syncthreads();
+    phase_mark(tmark, 17);
+    // 2. level-1 slots; vals (aliasing the staging, idle now) set to the identity
+    if (IA) {
+      const int id = SemI<SR>::identity();
+      int4* v4 = reinterpret_cast<int4*>(vals);
+      for (int j = tid; j < (nout + 3) >> 2; j += BS) v4[j] = make_int4(id, id, id, id);
+    } else {
+      const double id = Sem<SR>::identity();
+      double2* v2 = reinterpret_cast<double2*>(vals);
+      for (int j = tid; j < (nout + 1) >> 1; j += BS) v2[j] = make_double2(id, id);
+    }
+    const int nslot = bitmap_group_ranks<BS, G1PT>(l1q, ng1, g1pre, tmp);
+    __syncthreads();
+    int sl[RK];
+#pragma unroll
+    for (int k = 0; k < RK; ++k) {
+      sl[k] = -1;
+      if (xr[k] >= 0) {
+        sl[k] = bitmap_rank(l1q, g1pre, xr[k] >> 5);
+        atomicOr(&l2[sl[k]], 1u << (xr[k] & 31));
+      }
+    }
+    __syncthreads();
+    phase_mark(tmark, 18);
+    // 3. ranks: level-2 group ranks, then every product's rank; accumulate and
+    // write the rows at their ranks (into level 1, which nothing reads now)
+    bitmap_group_ranks<BS, G2PT>(l2q, (nslot + 3) >> 2, g2pre, tmp);
+    __syncthreads();
+    {
+      int* rows = reinterpret_cast<int*>(l1);
+#pragma unroll
+      for (int k = 0; k < RK; ++k)
+        if (sl[k] >= 0) {
+          const int rk = bitmap_rank(l2q, g2pre, (sl[k] << 5) | (xr[k] & 31));
+          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk, xv[k]);
+          else Sem<SR>::lds_acc(&vals[rk], xv[k]);
+          rows[rk] = lo + xr[k];
+        }
+    }
+    if (has_next) fetch2(nrec);
+    __syncthreads();
+    phase_mark(tmark, 19);
+    // 4. rows and values in rank order: coalesced copies
+    {
+      const int* rows = reinterpret_cast<const int*>(l1);
+      for (int j = tid; j < nout; j += BS) {
+        out_ir[obase + j] = rows[j];
+        st_emit(&out_val[obase + j], IA ? (double)reinterpret_cast<const int*>(vals)[j] : vals[j]);
+      }
+    }
+    if ((c_dbg & 32) && tid == 0) {
+      atomicAdd(&g_stat[10], (unsigned long long)total);
+      atomicAdd(&g_stat[11], (unsigned long long)nout);
+    }
+    __syncthreads();
     phase_mark(tmark, 20);
     if (!has_next) break;
     i = inext;
@@ -3150,6 +3421,29 @@ static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, cons
 // hash-mode single-panel slabs of more than this many nonzeros run as rank
 // slabs (scale 24: 400 / 1000 measured 3789 / 3825 vs 3795 ms; scale 22 flat)
 constexpr int RANK_SLABS_MIN = 683;
+// panel-group slabs of more than this many nonzeros run as group rank slabs
+constexpr int GRANK_SLABS_MIN = 683;
+
+template <int SR, int NCAP>
+static void launch_slab_grank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
+                              const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
+  if (n <= 0) return;
+  constexpr int L = SlabGRankLds<NCAP, RANK_BS>::BYTES;
+  DBuf<int> queue(1);
+  CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
+  auto go = [&](auto k, const auto* valA) {
+    set_lds(k, L);
+    const int per_cu = blocks_per_cu(k, RANK_BS, L);
+    const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
+                       A.ir, valA, C.ir, C.val);
+  };
+  if (bp.iacc) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRV, true>, bp.valAp);
+  else if (bp.valAp) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRV, false>, bp.valAp);
+  else if (bp.valAd) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRVD, false>, bp.valAd);
+  else go(k_num_slab_grank<SR, NCAP, RANK_BS, double, false>, A.val);
+  df.take(queue);
+}
 
 // ncls[c] slabs of class c, stored consecutively in `list` (k_slab_fill)
 
@@ -3180,6 +3474,8 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_rank<SR, 4096>(at[SLAB_RANK0 + 2], ncls[SLAB_RANK0 + 2], bp, A, B, C, s, df);
   launch_slab_rank<SR, 2048>(at[SLAB_RANK0 + 1], ncls[SLAB_RANK0 + 1], bp, A, B, C, s, df);
   launch_slab_rank<SR, 1024>(at[SLAB_RANK0], ncls[SLAB_RANK0], bp, A, B, C, s, df);
+  launch_slab_grank<SR, 4096>(at[SLAB_GRANK0 + 1], ncls[SLAB_GRANK0 + 1], bp, A, B, C, s, df);
+  launch_slab_grank<SR, 2048>(at[SLAB_GRANK0], ncls[SLAB_GRANK0], bp, A, B, C, s, df);
 
 }
 
@@ -4120,12 +4416,16 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     DBuf<int> counters(2 * NK + SLAB_NCLS);  // counts[NK] | cursor[NK] | class totals
     CBG_HIP(hipMemsetAsync(counters.p, 0, (2 * NK + SLAB_NCLS) * sizeof(int), s));
     const int rank_span = 1 << bp.plog, rank_min = RANK_SLABS_MIN;
+    // (CBG_GRANK_MIN, read per call: group slabs of more nonzeros than this run
+    // as group rank slabs; -1 none)
+    const char* egm = getenv("CBG_GRANK_MIN");
+    const int grank_min = egm ? (atoi(egm) < 0 ? INT32_MAX : atoi(egm)) : GRANK_SLABS_MIN;
     hipLaunchKernelGGL(k_slab_count, dim3(nblk(nbig, 256)), dim3(256), NK * sizeof(int), s, nbig, bp.R, bp.nslab.p,
-                       bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p);
+                       bp.cnt_br.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, grank_min, counters.p);
     hipLaunchKernelGGL(k_slab_bases, dim3(1), dim3(64), 0, s, bp.R, counters.p, counters.p + NK,
                        counters.p + 2 * NK);
     hipLaunchKernelGGL(k_slab_fill, dim3(nblk(nbig, 256)), dim3(256), 2 * NK * sizeof(int), s, nbig, bp.R,
-                       bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, counters.p + NK, slist.p,
+                       bp.nslab.p, bp.desc.p, SLAB_SMALL_CAP, rank_span, rank_min, grank_min, counters.p + NK, slist.p,
                        bp.perm_big, B.cp, colptr.p,
                        bp.gbm_slot.p, bp.plog, A.m, bp.pcoff.p);
     int* ncls_h = reinterpret_cast<int*>(host_stage(STAGE_SLABS));
@@ -4143,14 +4443,15 @@ void local_spgemm_impl(const cbg_tile& A, const cbg_tile& B, int semiring, cbg_t
     work[bp.all_kept ? CBG_WORK_BITMAP_LARGE_KEPT : CBG_WORK_BITMAP_LARGE_MARK] = ncls[1];
     for (int k = 0; k < SLAB_HASH_NCLS; ++k) work[CBG_WORK_HASH0 + k] = ncls[2 + k];
     for (int k = 0; k < SLAB_RANK_NCLS; ++k) work[CBG_WORK_RANK0 + k] = ncls[SLAB_RANK0 + k];
+    for (int k = 0; k < SLAB_GRANK_NCLS; ++k) work[CBG_WORK_GRANK0 + k] = ncls[SLAB_GRANK0 + k];
     static const int dbg = getenv("CBG_DBG") ? atoi(getenv("CBG_DBG")) : 0;
     if (dbg & 16)
     {
       static const int ht[SLAB_HASH_NCLS] = {CBG_HASH_TABLES};
       std::fprintf(stderr, "[cbg slabs] bitmap small %d large %d | hash", ncls[0], ncls[1]);
       for (int k = 0; k < SLAB_HASH_NCLS; ++k) std::fprintf(stderr, " T%d %d", ht[k], ncls[2 + k]);
-      std::fprintf(stderr, " | rank N1024 %d N2048 %d N4096 %d", ncls[SLAB_RANK0], ncls[SLAB_RANK0 + 1],
-                   ncls[SLAB_RANK0 + 2]);
+      std::fprintf(stderr, " | rank N1024 %d N2048 %d N4096 %d | group rank N2048 %d N4096 %d", ncls[SLAB_RANK0],
+                   ncls[SLAB_RANK0 + 1], ncls[SLAB_RANK0 + 2], ncls[SLAB_GRANK0], ncls[SLAB_GRANK0 + 1]);
       std::fprintf(stderr, "\n");
     }
   }

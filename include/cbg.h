@@ -192,7 +192,8 @@ enum {
   CBG_WORK_HASH_BIN_COLUMNS = 22,
   CBG_WORK_WAVE_BIN_COLUMNS = 23,
   CBG_WORK_IACC = 24, /* multiplies whose slabs accumulated exact integers in int32 */
-  CBG_WORK_N = 25
+  CBG_WORK_GRANK0 = 25, /* + k: panel-group rank slabs of <= 2048, 4096 nonzeros */
+  CBG_WORK_N = 27
 };
 int cbg_last_work_stats(int64_t* counts, int n);
 /* last call's multiway merges (MergeAll / MultiwayMerge): partial entries in,
