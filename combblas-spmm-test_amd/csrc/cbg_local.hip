@@ -2649,7 +2649,6 @@ constexpr int RANK_BS = 512;
 // group rank slabs (k_num_slab_grank): spans <= 2^22 rows (level 1: a bit per
 // 32 rows, <= 4096 words), <= GRANK_PMAX products (>= sym_group's 2/3 of GROUP_T)
 constexpr int GRANK_SPAN_LOG = 22;
-constexpr int GRANK_L1W = 1 << (GRANK_SPAN_LOG - 10);
 constexpr int GRANK_PMAX = 6144;
 static_assert((SLAB_WORDS > GROUP_T ? SLAB_WORDS : GROUP_T) * CBG_SYM_LOAD_DEN <= GRANK_PMAX * CBG_SYM_LOAD_NUM,
               "a panel group's products (sym_group: table <= hwords at load NUM/DEN) fit a group rank slab");
@@ -2863,28 +2862,30 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
 //      first rank;
 //   3. a product's rank = its slot's rank + the bits below it in the word;
 //      the products accumulate at their ranks and write their rows at them
-//      (into level 1's words, idle by then): C's rows and values come out in
-//      order with coalesced copies.
+//      (into level 1's words, idle by then, when they fit): C's rows and
+//      values come out in order with coalesced copies.
 // Against the hash slab (a returning CAS chain per product, then a bucket
 // counting sort of the table) this is two ds_or, two lookups and the
 // semiring's atomic per product.
-template <int NCAP, int BS>
+template <int NCAP, int BS, int SPANLOG, int PMAX>
 struct SlabGRankLds {
-  // ust: seg16[GRANK_PMAX] u16 | srec[BS]; from step 2 on vals[NCAP]
-  // l1[GRANK_L1W] (level 1; then C's rows) | g1pre[GRANK_L1W/4] u16 |
-  // l2[NCAP] | g2pre[NCAP/4] u16 | tmp[BS/64+4]
-  static constexpr int SEG_BYTES = GRANK_PMAX * 2;
+  // ust: seg16[PMAX] u16 | srec[BS]; from step 2 on vals[NCAP]
+  // l1[L1W] (level 1; then C's rows when NCAP <= L1W) | g1pre[L1W/4] u16 |
+  // l2[NCAP] | g2pre[NCAP/4] u16 | rows[NCAP] (when NCAP > L1W) | tmp[BS/64+4]
+  static constexpr int L1W = 1 << (SPANLOG - 10);
+  static constexpr bool ROWS_IN_L1 = NCAP <= L1W;
+  static constexpr int SEG_BYTES = PMAX * 2;
   static constexpr int UST = NCAP * 8 > SEG_BYTES + BS * 16 ? NCAP * 8 : SEG_BYTES + BS * 16;
   static constexpr int L1_OFF = UST;
-  static constexpr int G1_OFF = L1_OFF + GRANK_L1W * 4;
-  static constexpr int L2_OFF = G1_OFF + (GRANK_L1W / 4) * 2;
+  static constexpr int G1_OFF = L1_OFF + L1W * 4;
+  static constexpr int L2_OFF = G1_OFF + (L1W / 4 * 2 + 15) / 16 * 16;
   static constexpr int G2_OFF = L2_OFF + NCAP * 4;
-  static constexpr int TMP_OFF = G2_OFF + (NCAP / 4) * 2;
+  static constexpr int ROWS_OFF = G2_OFF + (NCAP / 4) * 2;
+  static constexpr int TMP_OFF = ROWS_OFF + (ROWS_IN_L1 ? 0 : NCAP * 4);
   static constexpr int BYTES = TMP_OFF + (BS / WAVE + 4) * 4;
   static_assert(SEG_BYTES % 16 == 0 && L1_OFF % 16 == 0 && G1_OFF % 16 == 0 && L2_OFF % 16 == 0 &&
-                    G2_OFF % 16 == 0 && TMP_OFF % 16 == 0,
+                    G2_OFF % 16 == 0 && ROWS_OFF % 16 == 0 && TMP_OFF % 16 == 0,
                 "group rank slab LDS alignment");
-  static_assert(NCAP <= GRANK_L1W, "a slab's rows (<= NCAP) are written into level 1's words");
 };
 // the rank of bit b of a bitmap: its 4-word group's rank + the bits below it
 __device__ __forceinline__ int bitmap_rank(const uint4* bm4, const unsigned short* gpre, int b) {
@@ -2931,17 +2932,18 @@ __device__ __forceinline__ int bitmap_group_ranks(const uint4* bm4, int ng, unsi
   }
   return tot;
 }
-template <int SR, int NCAP, int BS, typename VA, bool IA>
+template <int SR, int NCAP, int BS, int SPANLOG, int PMAX, typename VA, bool IA>
 __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict__ list, int n,
                                                        int* __restrict__ queue, int plog,
                                                        const int32_t* __restrict__ irB,
                                                        const double* __restrict__ valB, PMap pm,
                                                        const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                                        int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
-  using L = SlabGRankLds<NCAP, BS>;
+  using L = SlabGRankLds<NCAP, BS, SPANLOG, PMAX>;
   constexpr int NW = BS / WAVE;
-  constexpr int RK = GRANK_PMAX / BS;        // products per thread
-  constexpr int G1PT = (GRANK_L1W / 4) / BS;  // level-1 groups per thread in its scan
+  constexpr int RK = PMAX / BS;  // products per thread
+  static_assert(PMAX % BS == 0, "products per thread");
+  constexpr int G1PT = (L::L1W / 4 + BS - 1) / BS < 2 ? 2 : (L::L1W / 4 + BS - 1) / BS;  // level-1 groups per thread
   constexpr int G2PT = (NCAP / 4 + BS - 1) / BS < 2 ? 2 : (NCAP / 4 + BS - 1) / BS;
   static_assert(G1PT >= 2 && G1PT % 2 == 0 && G2PT % 2 == 0, "group rank scans: pairs of u16 ranks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2970,7 +2972,11 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
   // A(:,k)'s run over the group's panels r .. r1: the first panel's start to
   // the last one's end
   auto fetch2 = [&](const SlabRec& r) {
-    if (tid < r.nb) p_ce = make_int2(pm.at(r.r, p_ir).x, pm.at((r.hi - 1) >> plog, p_ir).y);
+    if (tid < r.nb) {
+      const int r1 = (r.hi - 1) >> plog;
+      p_ce = pm.at(r.r, p_ir);
+      if (r1 != r.r) p_ce.y = pm.at(r1, p_ir).y;
+    }
   };
   SlabRec rec = list[i];
   int qnext = 0;
@@ -2988,7 +2994,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
     const int64_t obase = rec.obase;
     for (int g = tid; g < ng1; g += BS) l1q[g] = make_uint4(0u, 0u, 0u, 0u);
     for (int g = tid; g < (nout + 3) >> 2; g += BS) l2q[g] = make_uint4(0u, 0u, 0u, 0u);
-    for (int g = tid; g < GRANK_PMAX / 8; g += BS) reinterpret_cast<uint4*>(seg16)[g] = make_uint4(0u, 0u, 0u, 0u);
+    for (int g = tid; g < PMAX / 8; g += BS) reinterpret_cast<uint4*>(seg16)[g] = make_uint4(0u, 0u, 0u, 0u);
     const int len = tid < rec.nb ? p_ce.y - p_ce.x : 0;
     int total;
     const int ex = block_excl_scan<BS>(len, tmp, &total);  // (its barriers order the zeroing above)
@@ -3056,7 +3062,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
     bitmap_group_ranks<BS, G2PT>(l2q, (nslot + 3) >> 2, g2pre, tmp);
     __syncthreads();
     {
-      int* rows = reinterpret_cast<int*>(l1);
+      int* rows = reinterpret_cast<int*>(smem + (L::ROWS_IN_L1 ? L::L1_OFF : L::ROWS_OFF));
 #pragma unroll
       for (int k = 0; k < RK; ++k)
         if (sl[k] >= 0) {
@@ -3071,7 +3077,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
     phase_mark(tmark, 19);
     // 4. rows and values in rank order: coalesced copies
     {
-      const int* rows = reinterpret_cast<const int*>(l1);
+      const int* rows = reinterpret_cast<const int*>(smem + (L::ROWS_IN_L1 ? L::L1_OFF : L::ROWS_OFF));
       for (int j = tid; j < nout; j += BS) {
         out_ir[obase + j] = rows[j];
         st_emit(&out_val[obase + j], IA ? (double)reinterpret_cast<const int*>(vals)[j] : vals[j]);
@@ -3424,11 +3430,11 @@ constexpr int RANK_SLABS_MIN = 683;
 // panel-group slabs of more than this many nonzeros run as group rank slabs
 constexpr int GRANK_SLABS_MIN = 683;
 
-template <int SR, int NCAP>
+template <int SR, int NCAP, int SPANLOG = GRANK_SPAN_LOG, int PMAX = GRANK_PMAX>
 static void launch_slab_grank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
                               const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  constexpr int L = SlabGRankLds<NCAP, RANK_BS>::BYTES;
+  constexpr int L = SlabGRankLds<NCAP, RANK_BS, SPANLOG, PMAX>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   auto go = [&](auto k, const auto* valA) {
@@ -3438,10 +3444,10 @@ static void launch_slab_grank(const SlabRec* list, int n, const BigPlan& bp, con
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(RANK_BS), L, s, list, n, queue.p, bp.plog, B.ir, B.val, bp.pm(),
                        A.ir, valA, C.ir, C.val);
   };
-  if (bp.iacc) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRV, true>, bp.valAp);
-  else if (bp.valAp) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRV, false>, bp.valAp);
-  else if (bp.valAd) go(k_num_slab_grank<SR, NCAP, RANK_BS, PackedRVD, false>, bp.valAd);
-  else go(k_num_slab_grank<SR, NCAP, RANK_BS, double, false>, A.val);
+  if (bp.iacc) go(k_num_slab_grank<SR, NCAP, RANK_BS, SPANLOG, PMAX, PackedRV, true>, bp.valAp);
+  else if (bp.valAp) go(k_num_slab_grank<SR, NCAP, RANK_BS, SPANLOG, PMAX, PackedRV, false>, bp.valAp);
+  else if (bp.valAd) go(k_num_slab_grank<SR, NCAP, RANK_BS, SPANLOG, PMAX, PackedRVD, false>, bp.valAd);
+  else go(k_num_slab_grank<SR, NCAP, RANK_BS, SPANLOG, PMAX, double, false>, A.val);
   df.take(queue);
 }
 
@@ -3471,6 +3477,9 @@ static void launch_slabs(const SlabRec* list, const int* ncls, const BigPlan& bp
   launch_slab_hash<SR, 4096, 512>(at[8], ncls[8], bp, A, B, C, hs(6), df);
   launch_slab_hash<SR, 6144, 512>(at[9], ncls[9], bp, A, B, C, hs(7), df);
   launch_slab_hash<SR, 8192, 512>(at[10], ncls[10], bp, A, B, C, hs(8), df);
+  // (the single-panel rank slabs by the two-level rank of the group slabs, 1
+  // KiB of level 1 for 2^18 rows and 2-3x the blocks per CU: 352.1 vs 344.0 ms
+  // at scale 22 -- the second lookup costs more than the occupancy buys)
   launch_slab_rank<SR, 4096>(at[SLAB_RANK0 + 2], ncls[SLAB_RANK0 + 2], bp, A, B, C, s, df);
   launch_slab_rank<SR, 2048>(at[SLAB_RANK0 + 1], ncls[SLAB_RANK0 + 1], bp, A, B, C, s, df);
   launch_slab_rank<SR, 1024>(at[SLAB_RANK0], ncls[SLAB_RANK0], bp, A, B, C, s, df);

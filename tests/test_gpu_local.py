@@ -1194,6 +1194,7 @@ def test_random_values_scale20_vs_oracle(cbg, sr):
         assert w[k] > 0, (k, w)
     assert sum(w["rank_N%d" % n] for n in (1024, 2048, 4096)) > 0, w
     assert sum(w["hash_T%d" % t] for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)) > 0, w
+    assert sum(w["group_rank_N%d" % n] for n in (2048, 4096)) > 0, w
     Ch = C.to_host()
     C.free()
     ref = oracle_local(Ah, Bh, sr)
@@ -1236,7 +1237,7 @@ def test_random_values_scale22_pieces_vs_oracle(cbg):
     the tile (B = A's columns [p n/512, (p+1) n/512)) for 10 pieces spread over the
     columns, the high-id end included.  Every piece has big columns over 16 panels:
     bitmap pairs (single- and multi-slab), rank slabs (single-panel sparse pairs),
-    hash slabs (panel groups).  Entry by entry against the CPU oracle: plus-times
+    two-level rank slabs (panel groups), hash slabs (the smallest sparse slabs).  Entry by entry against the CPU oracle: plus-times
     within 1e-12 (|A||B|)_ij; min-plus exact on three of the pieces
     (mtSpGEMM.h:362-440 semantics, Dcsc::operator== dcsc.cpp:472-510)."""
     n = 1 << 22
@@ -1268,11 +1269,52 @@ def test_random_values_scale22_pieces_vs_oracle(cbg):
     A.free()
     # every kernel family the docstring names ran with f64 values: symbolic units
     # and panel groups, both bitmap slab classes (kept bitmaps), all three rank
-    # classes, several hash-slab table sizes
+    # classes, both group rank classes, several hash-slab table sizes
     for k in ("sym_panel_units", "sym_group_units", "bitmap_small_kept", "bitmap_large_kept", "rank_N1024",
-              "rank_N2048", "rank_N4096"):
+              "rank_N2048", "rank_N4096", "group_rank_N2048", "group_rank_N4096"):
         assert work[k] > 0, (k, work)
-    assert sum(1 for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192) if work["hash_T%d" % t]) >= 3, work
+    assert sum(1 for t in (512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192) if work["hash_T%d" % t]) >= 2, work
+
+
+@pytest.mark.parametrize("grank_min", ["-1", "0"])
+def test_group_slabs_hash_or_rank_vs_oracle(cbg, grank_min):
+    """Panel-group slabs either way (CBG_GRANK_MIN, read per call): -1 sends every
+    group slab to the hash slabs (k_num_slab_hash, the larger tables among them), 0
+    every group slab of a span <= 2^22 to the two-level rank (k_num_slab_grank, the
+    small ones too).  Scale-20 R-MAT with U[-1,1) values times every 16th column
+    (R = 4 panels, groups of 2 and 4), both semirings, entry by entry against the
+    oracle (plus-times within 1e-12 (|A||B|)_ij, min-plus exact)."""
+    import os
+    old = os.environ.get("CBG_GRANK_MIN")
+    os.environ["CBG_GRANK_MIN"] = grank_min
+    try:
+        A = cbg.rmat_tile(20, 16).set_random_values()
+        Ah = A.to_host()
+        Bh = _cols_host(Ah, lambda j: j % 16 == 0)
+        B = cbg.Tile.from_dict(Bh)
+        for sr in ("plus", "minplus"):
+            C = cbg.LocalHybridSpGEMM(A, B, sr)
+            w = cbg.last_work_stats()
+            g = w["group_rank_N2048"] + w["group_rank_N4096"]
+            big_hash = sum(w["hash_T%d" % t] for t in (2048, 3072, 4096, 6144, 8192))
+            if grank_min == "-1":
+                assert g == 0 and big_hash > 0, w
+            else:
+                assert g > 0 and big_hash == 0, w
+            Ch = C.to_host()
+            C.free()
+            ref = oracle_local(Ah, Bh, sr)
+            if sr == "plus":
+                assert_tiles_equal(Ch, ref, rtol=RTOL, bound=oracle_local(abs_tile(Ah), abs_tile(Bh))["val"])
+            else:
+                assert_tiles_equal(Ch, ref)
+        A.free()
+        B.free()
+    finally:
+        if old is None:
+            del os.environ["CBG_GRANK_MIN"]
+        else:
+            os.environ["CBG_GRANK_MIN"] = old
 
 
 def _subprocess_local(env, code, timeout=600):
