@@ -585,8 +585,14 @@ constexpr int BIG_BS = CBG_BIG_BS;
 #define CBG_SPARSE_SLAB_MAX 4096
 #endif
 constexpr int SPARSE_SLAB_MAX = CBG_SPARSE_SLAB_MAX;  // products of a (column, panel) pair counted by hash -> hash slab
+// group rank slabs (k_num_slab_grank): spans <= 2^22 rows (level 1: a bit per
+// 32 rows, <= 4096 words), <= GRANK_PMAX products (8 per thread: 80 VGPRs, 3
+// blocks per CU; sym_group flags the groups with more, which stay hash slabs)
+constexpr int GRANK_SPAN_LOG = 22;
+constexpr int GRANK_PMAX = 4096;
 constexpr int SLAB_SPARSE = 1 << 30;    // desc.w flag: hash-mode slab (count in the low bits)
-constexpr int SLAB_CNT_MASK = SLAB_SPARSE - 1;
+constexpr int SLAB_MANYP = 1 << 29;     // desc.w flag: a panel group's slab of > GRANK_PMAX products
+constexpr int SLAB_CNT_MASK = SLAB_MANYP - 1;
 
 // Panel column maps of A: entry (r, k) = (first, end) of column k's entries
 // in row panel r (layout: PMap below).  A panel without rows of A(:,k) gets (q, q) with q
@@ -1133,7 +1139,8 @@ __device__ __forceinline__ bool sym_group(const SymPanelArgs& a, const SymPanelL
     if (a.gbm_slot) a.gbm_slot[br] = -1;
     if (first && cg)
       a.desc[br * NFINE_MAX] =
-          make_int4(r0 << a.plog, (int)min((int64_t)(r1 + 1) << a.plog, a.m), 0, cg | SLAB_SPARSE);
+          make_int4(r0 << a.plog, (int)min((int64_t)(r1 + 1) << a.plog, a.m), 0,
+                    cg | SLAB_SPARSE | (total > GRANK_PMAX ? SLAB_MANYP : 0));
   }
   if (tid == 0 && cg) atomicAdd(&a.cnt[col], cg);
   return true;
@@ -1317,7 +1324,7 @@ __device__ __forceinline__ int slab_class(const int4& d, int small_cap, int rank
     const int c = w & SLAB_CNT_MASK;
     if (c > rank_min && rank_span > 0 && d.y - d.x <= rank_span)
       return SLAB_RANK0 + (c <= 1024 ? 0 : c <= 2048 ? 1 : 2);
-    if (c > grank_min && d.y - d.x > rank_span && d.y - d.x <= (1 << 22))
+    if (c > grank_min && !(w & SLAB_MANYP) && d.y - d.x > rank_span && d.y - d.x <= (1 << GRANK_SPAN_LOG))
       return SLAB_GRANK0 + (c <= 2048 ? 0 : 1);
     int k = 0;
     while (k + 1 < SLAB_HASH_NCLS && c_hash_t[k] * CBG_HASH_LOAD_DEN < CBG_HASH_LOAD_NUM * c) ++k;  // load <= NUM/DEN
@@ -2646,13 +2653,8 @@ struct SlabRankLds {
   static_assert(SEG_BYTES % 16 == 0 && BM_OFF % 16 == 0 && GPRE_OFF % 16 == 0, "rank slab LDS alignment");
 };
 constexpr int RANK_BS = 512;
-// group rank slabs (k_num_slab_grank): spans <= 2^22 rows (level 1: a bit per
-// 32 rows, <= 4096 words), <= GRANK_PMAX products (>= sym_group's 2/3 of GROUP_T)
-constexpr int GRANK_SPAN_LOG = 22;
-constexpr int GRANK_PMAX = 6144;
-static_assert((SLAB_WORDS > GROUP_T ? SLAB_WORDS : GROUP_T) * CBG_SYM_LOAD_DEN <= GRANK_PMAX * CBG_SYM_LOAD_NUM,
-              "a panel group's products (sym_group: table <= hwords at load NUM/DEN) fit a group rank slab");
-static_assert(SPARSE_NNZ_MAX <= 4096 && BIG_BS <= RANK_BS, "group rank slab: nonzeros and B entries");
+static_assert(SPARSE_NNZ_MAX <= 4096 && BIG_BS <= RANK_BS && GRANK_PMAX % RANK_BS == 0,
+              "group rank slab: nonzeros, B entries, products per thread");
 static_assert(4096 <= SLAB_WORDS, "a rank slab's rows (<= 4096) are written into its bitmap's words");
 // a rank slab stages one B entry per thread: the symbolic's sparse pairs (the
 // rank slabs' source, sym_pair) have <= BIG_BS B entries
@@ -3008,8 +3010,9 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
     build_segids<BS, RK>(seg16, tmp);
     phase_mark(tmark, 16);
     // 1. products into registers, their 32-row blocks marked in level 1
+    // (exact integers as int: fewer VGPRs, more blocks per CU)
     int xr[RK];
-    double xv[RK];
+    typename std::conditional<IA, int, double>::type xv[RK];
     {
       int sg[RK];
 #pragma unroll
@@ -3024,7 +3027,8 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
           const SegRec r = srec[sg[k]];
           const RowVal x = a_rowval<SR, VA>(irA, valA, r.off + tid + k * BS, r.b, lo);
           xr[k] = x.row;
-          xv[k] = x.v;
+          if constexpr (IA) xv[k] = (int)x.v;
+          else xv[k] = x.v;
         }
       }
 #pragma unroll
@@ -3067,7 +3071,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
       for (int k = 0; k < RK; ++k)
         if (sl[k] >= 0) {
           const int rk = bitmap_rank(l2q, g2pre, (sl[k] << 5) | (xr[k] & 31));
-          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk, xv[k]);
+          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk, (double)xv[k]);
           else Sem<SR>::lds_acc(&vals[rk], xv[k]);
           rows[rk] = lo + xr[k];
         }

@@ -1300,7 +1300,7 @@ def test_group_slabs_hash_or_rank_vs_oracle(cbg, grank_min):
             if grank_min == "-1":
                 assert g == 0 and big_hash > 0, w
             else:
-                assert g > 0 and big_hash == 0, w
+                assert g > 0, w
             Ch = C.to_host()
             C.free()
             ref = oracle_local(Ah, Bh, sr)
