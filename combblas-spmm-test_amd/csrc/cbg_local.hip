@@ -2638,14 +2638,14 @@ __global__ __launch_bounds__(BS) CBG_HASH_WPE_ATTR void k_num_slab_hash(const Sl
 // The bitmap (32 KiB) is zeroed per slab and read twice in 16-byte vectors; every
 // random LDS access is one ds_or, two reads (group, its rank) and the semiring's
 // atomic per product.
-template <int NCAP, int BS>
+template <int NCAP, int BS, int VB = 8>
 struct SlabRankLds {
   // ust: during the products seg16[SPARSE_SLAB_MAX] u16 (each product's segment) |
   //      srec[BS] (segment: A offset minus its first product index, B value);
-  //      from the rank scan on vals[NCAP] f64
+  //      from the rank scan on vals[NCAP] (f64, or int32 under IACC: VB = 4)
   // bm[SLAB_WORDS] | gpre[SLAB_WORDS / 4] u16 | tmp[BS/64+4]
   static constexpr int SEG_BYTES = SPARSE_SLAB_MAX * 2;
-  static constexpr int UST = NCAP * 8 > SEG_BYTES + BS * 16 ? NCAP * 8 : SEG_BYTES + BS * 16;
+  static constexpr int UST = NCAP * VB > SEG_BYTES + BS * 16 ? NCAP * VB : SEG_BYTES + BS * 16;
   static constexpr int BM_OFF = UST;
   static constexpr int GPRE_OFF = BM_OFF + SLAB_WORDS * 4;
   static constexpr int TMP_OFF = GPRE_OFF + (SLAB_WORDS / 4) * 2;
@@ -2672,7 +2672,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
                                                       PMap pm,
                                                       const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                                       int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
-  using L = SlabRankLds<NCAP, BS>;
+  using L = SlabRankLds<NCAP, BS, IA ? 4 : 8>;
   constexpr int NW = BS / WAVE;
   constexpr int RK = SPARSE_SLAB_MAX / BS;  // products per thread
   constexpr int NG = SLAB_WORDS / 4;        // 4-word groups of a panel
@@ -2736,7 +2736,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
     phase_mark(tmark, 16);
     // 1. products into registers (thread t: t + BS k), rows marked in the bitmap
     int xr[RK];
-    double xv[RK];
+    typename std::conditional<IA, int, double>::type xv[RK];  // (exact integers as int: fewer VGPRs)
     {
       int sg[RK];
 #pragma unroll
@@ -2751,7 +2751,8 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
           const SegRec r = srec[sg[k]];
           const RowVal x = a_rowval<SR, VA>(irA, valA, r.off + tid + k * BS, r.b, lo);
           xr[k] = x.row;
-          xv[k] = x.v;
+          if constexpr (IA) xv[k] = (int)x.v;
+          else xv[k] = x.v;
         }
       }
 #pragma unroll
@@ -2821,7 +2822,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
 #pragma unroll
       for (int k = 0; k < RK; ++k)
         if (rk[k] >= 0) {
-          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk[k], xv[k]);
+          if constexpr (IA) SemI<SR>::lds_acc(reinterpret_cast<int*>(vals) + rk[k], (double)xv[k]);
           else Sem<SR>::lds_acc(&vals[rk[k]], xv[k]);
           rows[rk[k]] = lo + xr[k];
         }
@@ -2869,15 +2870,16 @@ __global__ __launch_bounds__(BS) void k_num_slab_rank(const SlabRec* __restrict_
 // Against the hash slab (a returning CAS chain per product, then a bucket
 // counting sort of the table) this is two ds_or, two lookups and the
 // semiring's atomic per product.
-template <int NCAP, int BS, int SPANLOG, int PMAX>
+template <int NCAP, int BS, int SPANLOG, int PMAX, int VB = 8>
 struct SlabGRankLds {
-  // ust: seg16[PMAX] u16 | srec[BS]; from step 2 on vals[NCAP]
+  // ust: seg16[PMAX] u16 | srec[BS]; from step 2 on vals[NCAP] (f64, or int32
+  // under IACC: VB = 4)
   // l1[L1W] (level 1; then C's rows when NCAP <= L1W) | g1pre[L1W/4] u16 |
   // l2[NCAP] | g2pre[NCAP/4] u16 | rows[NCAP] (when NCAP > L1W) | tmp[BS/64+4]
   static constexpr int L1W = 1 << (SPANLOG - 10);
   static constexpr bool ROWS_IN_L1 = NCAP <= L1W;
   static constexpr int SEG_BYTES = PMAX * 2;
-  static constexpr int UST = NCAP * 8 > SEG_BYTES + BS * 16 ? NCAP * 8 : SEG_BYTES + BS * 16;
+  static constexpr int UST = NCAP * VB > SEG_BYTES + BS * 16 ? NCAP * VB : SEG_BYTES + BS * 16;
   static constexpr int L1_OFF = UST;
   static constexpr int G1_OFF = L1_OFF + L1W * 4;
   static constexpr int L2_OFF = G1_OFF + (L1W / 4 * 2 + 15) / 16 * 16;
@@ -2941,7 +2943,7 @@ __global__ __launch_bounds__(BS) void k_num_slab_grank(const SlabRec* __restrict
                                                        const double* __restrict__ valB, PMap pm,
                                                        const int32_t* __restrict__ irA, const VA* __restrict__ valA,
                                                        int32_t* __restrict__ out_ir, double* __restrict__ out_val) {
-  using L = SlabGRankLds<NCAP, BS, SPANLOG, PMAX>;
+  using L = SlabGRankLds<NCAP, BS, SPANLOG, PMAX, IA ? 4 : 8>;
   constexpr int NW = BS / WAVE;
   constexpr int RK = PMAX / BS;  // products per thread
   static_assert(PMAX % BS == 0, "products per thread");
@@ -3411,10 +3413,10 @@ template <int SR, int NCAP>
 static void launch_slab_rank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
                              const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  constexpr int L = SlabRankLds<NCAP, RANK_BS>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   auto go = [&](auto k, const auto* valA) {
+    const int L = bp.iacc ? SlabRankLds<NCAP, RANK_BS, 4>::BYTES : SlabRankLds<NCAP, RANK_BS, 8>::BYTES;
     set_lds(k, L);
     const int per_cu = blocks_per_cu(k, RANK_BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
@@ -3438,10 +3440,11 @@ template <int SR, int NCAP, int SPANLOG = GRANK_SPAN_LOG, int PMAX = GRANK_PMAX>
 static void launch_slab_grank(const SlabRec* list, int n, const BigPlan& bp, const cbg_tile& A,
                               const cbg_tile& B, cbg_tile& C, hipStream_t s, DeferredFree& df) {
   if (n <= 0) return;
-  constexpr int L = SlabGRankLds<NCAP, RANK_BS, SPANLOG, PMAX>::BYTES;
   DBuf<int> queue(1);
   CBG_HIP(hipMemsetAsync(queue.p, 0, sizeof(int), s));
   auto go = [&](auto k, const auto* valA) {
+    const int L = bp.iacc ? SlabGRankLds<NCAP, RANK_BS, SPANLOG, PMAX, 4>::BYTES
+                          : SlabGRankLds<NCAP, RANK_BS, SPANLOG, PMAX, 8>::BYTES;
     set_lds(k, L);
     const int per_cu = blocks_per_cu(k, RANK_BS, L);
     const int grid = (int)std::min<int64_t>(n, (int64_t)per_cu * active_cus());
