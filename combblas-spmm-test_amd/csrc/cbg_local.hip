@@ -673,9 +673,14 @@ __global__ void k_colmap_panels_entries(const int32_t* __restrict__ perm_big, in
 // map hops of up to 16 panels and reads A's runs over the group contiguously.
 constexpr int GROUP_LOG_MAX = 6;      // groups of up to 64 panels (scale 24: R = 64 panels per column)
 #ifndef CBG_GROUP_PRODUCTS
-#define CBG_GROUP_PRODUCTS 3072
+#define CBG_GROUP_PRODUCTS 4096
 #endif
-constexpr int GROUP_PRODUCTS = CBG_GROUP_PRODUCTS;  // expected products of a group (launch class thresholds; with hash load 2/3: 1536/2048/4096 measured slower)
+// expected products of a group (launch class thresholds).  With hash-slab
+// numerics 3072 was best (1536/2048/4096 slower); with the group rank slabs
+// 4096 is: scale 22 317-321 ms vs 332 (3072), 323 (3584), 333 (4608), 357
+// (2048), 357 (5120), 393 (6144) -- past ~4096 expected products the groups
+// overflow the symbolic's table and the group rank slab's products
+constexpr int GROUP_PRODUCTS = CBG_GROUP_PRODUCTS;
 #ifndef CBG_SYM_WAVES_OF_UNITS  // persistent symbolic grid: resident blocks x this
 #define CBG_SYM_WAVES_OF_UNITS 32  // 1: -2 % (static stride meets hub-column imbalance); 16-32: +1 % at scale 22
 #endif
