@@ -3200,10 +3200,8 @@ constexpr int SYM_FUSED_LAST = CBG_SYM_FUSED_LAST;
 static int64_t big_flops(int64_t m) {
   static const char* e = getenv("CBG_BIG_FLOPS");
   // measured on R-MAT (scale 18/20): 4096 once hash slabs take the sparse
-  // (column, panel) pairs and the block hash bins emit by bucket sort; 1024
-  // since the panel groups' rank slabs (round 6, scale 22: 311.9 vs 317.0 ms,
-  // 512: 317.3, 256: 321.1; scale 18: 5.90-6.03 vs 6.17-6.20 ms)
-  int64_t b = e ? atoll(e) : 1024;
+  // (column, panel) pairs and the block hash bins emit by bucket sort
+  int64_t b = e ? atoll(e) : 4096;
   if (b < 64) b = 64;
   if (b > 4096) b = 4096;
   return b;
